@@ -1,0 +1,154 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+from oracle import milwrm_oracle as O
+
+
+def _nan_i8(a):
+    a = a.astype(np.float64)
+    a[a < 0] = np.nan
+    return a
+
+
+def test_non_zero_mean_and_batch_means(golden):
+    g = golden("mxif_small")
+    ests, pix = zip(*[O.non_zero_mean(r) for r in g["raw"]])
+    np.testing.assert_array_equal(np.array(ests), g["mean_estimators"])
+    np.testing.assert_array_equal(np.array(pix), g["pixels"])
+    bm = O.batch_means(ests, pix, list(g["batch_names"]))
+    np.testing.assert_array_equal(bm["b1"], g["batch_mean_b1"])
+    np.testing.assert_array_equal(bm["b2"], g["batch_mean_b2"])
+
+
+def test_lognorm_blur_matches_reference(golden):
+    g = golden("mxif_small")
+    bm = g["batch_mean_b1"]
+    x = O.gaussian_blur(O.log_normalize(g["raw"][0], bm), 2.0)
+    np.testing.assert_allclose(x, g["preprocessed0"], rtol=1e-12, atol=1e-14)
+    x2 = O.gaussian_blur(O.log_normalize(g["raw"][2], g["batch_mean_b2"]), 2.0)
+    np.testing.assert_allclose(x2, g["preprocessed2"], rtol=1e-12, atol=1e-14)
+
+
+def test_subsample_and_scaler(golden):
+    g = golden("mxif_small")
+    subs = []
+    for i, b in enumerate(["b1", "b1", "b2"]):
+        bm = g["batch_mean_b1"] if b == "b1" else g["batch_mean_b2"]
+        x = O.gaussian_blur(O.log_normalize(g["raw"][i], bm), 2.0)
+        s, idx = O.subsample_pixels(x, g["masks"][i], list(range(8)), 0.2)
+        subs.append(s)
+        if i == 0:
+            np.testing.assert_array_equal(idx, g["sub_idx0"])
+    X = np.vstack(subs)
+    mean, scale, _ = O.scaler_fit(X)
+    np.testing.assert_allclose(mean, g["scaler_mean"], rtol=1e-13)
+    np.testing.assert_allclose(scale, g["scaler_scale"], rtol=1e-13)
+    np.testing.assert_allclose(O.scaler_transform(X, mean, scale), g["cluster_data"], rtol=1e-11, atol=1e-12)
+
+
+def test_legacy_randint_restatement():
+    for M, fr in [(6540, 0.2), (1000, 0.5), (2**20, 0.01), (2**20 + 1, 0.01), (123457, 0.3)]:
+        np.random.seed(16)
+        ref = np.random.choice(M, int(M * fr))
+        mine = O.legacy_randint_masked(16, M, int(M * fr))
+        np.testing.assert_array_equal(mine, ref)
+
+
+def test_kmeans_plusplus_indices(golden):
+    g = golden("mxif_small")
+    X = g["cluster_data"]
+    Xc = X - X.mean(axis=0)
+    for k in (2, 3, 8, 13, 20):
+        _, idx = O.kmeans_plusplus(Xc, k, 18)
+        np.testing.assert_array_equal(idx, g["kpp_indices"][k, :k])
+
+
+def test_first_center_closed_form_vs_numpy():
+    for n in (1, 7, 6297, 100003, 2**20):
+        rs = np.random.RandomState(18)
+        ref = rs.choice(n, p=np.ones(n) / n)
+        u = np.random.RandomState(18).random_sample()
+        assert O.first_center_index(n, u) == ref
+
+
+def test_single_lloyd_step(golden):
+    g = golden("mxif_small")
+    X = g["cluster_data"]
+    Xc = X - X.mean(axis=0)
+    labels, cn, w, shift = O.lloyd_iter(Xc, g["lloyd1_centers_in"])
+    np.testing.assert_array_equal(labels, g["lloyd1_labels"])
+    np.testing.assert_allclose(cn, g["lloyd1_centers_out"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_array_equal(w, g["lloyd1_weights"])
+    np.testing.assert_allclose(shift, g["lloyd1_shift"], rtol=1e-11)
+
+
+def test_kmeans_fit_and_sweep(golden):
+    g = golden("mxif_small")
+    X = g["cluster_data"]
+    best_k, curve = O.choose_best_k(X, range(2, 21), 0.05, 18)
+    assert best_k == int(g["best_k"])
+    np.testing.assert_allclose([curve[k] for k in range(2, 21)], g["sweep_scaled_inertia"], rtol=1e-10)
+    r = O.kmeans_fit(X, int(g["k"]), 18)
+    np.testing.assert_array_equal(r["labels_"], g["labels"])
+    np.testing.assert_allclose(r["cluster_centers_"], g["centers"], rtol=1e-10, atol=1e-12)
+    assert r["n_iter_"] == int(g["n_iter"])
+    np.testing.assert_allclose(r["inertia_"], float(g["inertia"]), rtol=1e-10)
+
+
+def test_tissue_ids_and_confidence(golden):
+    g = golden("mxif_small")
+    centers, mean, scale = g["centers"], g["scaler_mean"], g["scaler_scale"]
+    for i, b in enumerate(["b1", "b1", "b2"]):
+        bm = g["batch_mean_b1"] if b == "b1" else g["batch_mean_b2"]
+        x = O.gaussian_blur(O.log_normalize(g["raw"][i], bm), 2.0)
+        t = O.tissue_ids(x, g["masks"][i], list(range(8)), centers, mean, scale)
+        np.testing.assert_array_equal(np.nan_to_num(t, nan=-1), np.nan_to_num(_nan_i8(g["tissue_IDs"][i]), nan=-1))
+        c, cm = O.confidence_mxif(x, g["masks"][i], list(range(8)), centers, mean, scale, t)
+        np.testing.assert_allclose(c, g["confidence_IDs"][i], rtol=1e-9, atol=1e-12, equal_nan=True)
+        np.testing.assert_allclose([cm[j] for j in range(len(centers))], g["confidence_score_df"][i],
+                                   rtol=1e-9, equal_nan=True)
+
+
+def test_pipeline_hard256(golden):
+    g = golden("mxif_hard256")
+    r = O.mxif_pipeline([g["raw"]], [g["mask"]], ["b"], list(range(30)), k=8)
+    np.testing.assert_allclose(r["kmeans"]["cluster_centers_"], g["centers"], rtol=1e-9, atol=1e-11)
+    assert r["kmeans"]["n_iter_"] == int(g["n_iter"])
+    np.testing.assert_allclose(r["kmeans"]["inertia_"], float(g["inertia"]), rtol=1e-10)
+    t = np.nan_to_num(r["tissue_IDs"][0], nan=-1).astype(np.int8)
+    np.testing.assert_array_equal(t, g["tissue_IDs"])
+    np.testing.assert_allclose(r["confidence_IDs"][0], g["confidence_IDs"], rtol=1e-6, equal_nan=True)
+
+
+def test_gaussian_edges_and_downsample(golden):
+    g = golden("preproc_edges")
+    for i in range(5):
+        out = O.gaussian_blur(g[f"gauss{i}_in"], float(g[f"gauss{i}_sigma"]))
+        np.testing.assert_allclose(out, g[f"gauss{i}_out"], rtol=1e-12, atol=1e-14)
+    for i in range(3):
+        f = int(g[f"down{i}_fact"])
+        np.testing.assert_allclose(O.block_reduce_mean(g[f"down{i}_in"], f), g[f"down{i}_out"], rtol=1e-14)
+        np.testing.assert_allclose(O.block_reduce_mean(g[f"down{i}_mask"], f), g[f"down{i}_mask_out"], rtol=1e-14)
+    np.testing.assert_allclose(O.log_normalize(g["lognorm_none_in"]), g["lognorm_none_out"], rtol=1e-14)
+
+
+def test_st_plumbing(golden):
+    import scipy.sparse as sp
+
+    g = golden("st_hex")
+    feats = []
+    for s in range(2):
+        n = g[f"pcs{s}"].shape[0]
+        A = sp.csr_matrix((np.ones(len(g[f"adj{s}_indices"])), g[f"adj{s}_indices"], g[f"adj{s}_indptr"]), shape=(n, n))
+        feats.append(O.blur_features_st(g[f"pcs{s}"], A))
+    X = np.vstack(feats)
+    mean, scale, _ = O.scaler_fit(X)
+    Xs = O.scaler_transform(X, mean, scale)
+    np.testing.assert_allclose(Xs, g["cluster_data"], rtol=1e-10, atol=1e-12)
+    r = O.kmeans_fit(Xs, int(g["k"]), 18)
+    np.testing.assert_array_equal(r["labels_"], g["labels"])
+    n0 = g["pcs0"].shape[0]
+    c0, _ = O.confidence_st(Xs[:n0], r["cluster_centers_"], r["labels_"][:n0])
+    np.testing.assert_allclose(c0, g["conf0"], rtol=1e-9)
