@@ -1,0 +1,177 @@
+/*
+ * milwrm_amd — C ABI of the MI355X-native MILWRM pixel-clustering hot path.
+ *
+ * Plain pointers and sizes only (no torch types).  Every pointer named d_* is
+ * device memory (HBM) owned by the caller; h_* is host memory.  `stream` is a
+ * hipStream_t passed as void*.  All launches are asynchronous on `stream`
+ * unless a function says it synchronises.  Workspace buffers (d_ws) are
+ * caller-allocated; their sizes come from the matching *_ws_bytes() query.
+ * The library never frees caller memory and never allocates inside a launch
+ * function.  Status: 0 = ok, < 0 = error; mw_last_error() gives the text.
+ *
+ * Reference interfaces replaced (file:line in codyheiser/MILWRM unless noted;
+ * sklearn/scipy paths are the pinned third-party engines the reference calls):
+ *   mw_nz_stats        img.calculate_non_zero_mean        MxIF.py:519-541
+ *   mw_lognorm         img.log_normalize                  MxIF.py:416-455
+ *   mw_blur            img.blurring('gaussian') → skimage.filters.gaussian →
+ *                      scipy.ndimage.gaussian_filter       MxIF.py:375-394
+ *   mw_block_mean      img.downsample → skimage block_reduce MxIF.py:494-517
+ *   mw_mask_rank,
+ *   mw_gather_rows     img.subsample_pixels (mask gather + fancy index)
+ *                                                          MxIF.py:457-492
+ *   mw_legacy_randint_* np.random.seed(16); np.random.choice(M, S)
+ *                                                          MxIF.py:484,490
+ *   mw_col_stats_finalize StandardScaler.fit               MILWRM.py:1742-1745
+ *   mw_kpp_*           sklearn _kmeans_plusplus            _kmeans.py:174-272
+ *   mw_lloyd_step,
+ *   mw_lloyd_reduce    sklearn lloyd_iter_chunked_dense    _k_means_lloyd.pyx:23-218
+ *   mw_farthest        sklearn _relocate_empty_clusters_dense _k_means_common.pyx:181-226
+ *   mw_assign_conf     KMeans.predict + estimate_confidence_score_mxif
+ *                                                          MILWRM.py:237-277, 389-450
+ */
+#ifndef MILWRM_AMD_H
+#define MILWRM_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define MW_OK 0
+#define MW_EINVAL (-1)      /* bad argument (ValueError on the Python side) */
+#define MW_EHIP (-2)        /* HIP runtime error */
+#define MW_EUNSUPPORTED (-3) /* shape/parameter outside what the kernels take */
+
+/* element types of image planes */
+#define MW_U8 0
+#define MW_U16 1
+#define MW_F32 2
+
+int mw_version(void);
+const char* mw_last_error(void);
+/* Number of streaming workgroups the reductions use for `n` rows; partial
+ * buffers are sized from it.  Fixed per n (not per device) so results are
+ * identical across runs and shard layouts. */
+int mw_stream_blocks(int64_t n);
+
+/* ---- img.calculate_non_zero_mean (MxIF.py:519-541) --------------------------
+ * HWC image of n_pix pixels x C channels.  Outputs per channel: sum of the
+ * non-zero values (fp64) and their count (int64).  Deterministic. */
+size_t mw_nz_stats_ws_bytes(int64_t n_pix, int C);
+int mw_nz_stats(const void* d_img, int dtype, int64_t n_pix, int C,
+                double* d_sum, int64_t* d_cnt, void* d_ws, void* stream);
+
+/* ---- img.log_normalize (MxIF.py:416-455) ------------------------------------
+ * out = log10(x * inv_mean[c] + pseudoval), HWC, fp32 out. */
+int mw_lognorm(const void* d_img, int dtype, int64_t n_pix, int C,
+               const float* d_inv_mean, float pseudoval, float* d_out, void* stream);
+
+/* ---- img.blurring('gaussian', sigma) (MxIF.py:375-394) ----------------------
+ * Separable Gaussian, per channel, edge-replicate ('nearest'), radius r =
+ * int(4*sigma+0.5) <= 32, taps h_w[0..2r] (scipy _gaussian_kernel1d).
+ * Optional fused log-normalise prologue when d_inv_mean != NULL.  HWC in,
+ * HWC fp32 out (out must not alias in).  r <= 12: single streaming pass
+ * (register ring); r > 12: two passes through d_ws (mw_blur_ws_bytes). */
+size_t mw_blur_ws_bytes(int H, int W, int C, int radius);
+int mw_blur(const void* d_img, int dtype, int H, int W, int C,
+            const float* d_inv_mean, float pseudoval,
+            const float* h_w, int radius, float* d_out, void* d_ws, void* stream);
+
+/* ---- img.downsample(fact, np.mean) (MxIF.py:494-517) ------------------------
+ * block mean over fact x fact, zero padded to a multiple of fact, pad zeros
+ * included.  HWC in, fp32 HWC out of ceil(H/f) x ceil(W/f) x C. */
+int mw_block_mean(const void* d_img, int dtype, int H, int W, int C, int fact,
+                  float* d_out, void* stream);
+
+/* ---- mask row-major rank → pixel (MxIF.py:486-488) --------------------------
+ * d_rank2pix[r] = flat index of the r-th pixel with mask != 0.  d_count gets
+ * the number of such pixels (int64 on device). */
+size_t mw_mask_rank_ws_bytes(int64_t n_pix);
+int mw_mask_rank(const uint8_t* d_mask, int64_t n_pix, uint32_t* d_rank2pix,
+                 int64_t* d_count, void* d_ws, void* stream);
+
+/* ---- subsample gather (MxIF.py:490-491) -------------------------------------
+ * X[j, f] = img[rank2pix[idx[j]], feat[f]] as fp32 rows (S x F), plus per
+ * block column statistics (count, mean, M2 in fp64) for StandardScaler.
+ * d_img is fp32 HWC with C channels. */
+size_t mw_gather_ws_bytes(int64_t S, int F);
+int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F,
+                   const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S,
+                   float* d_X, void* d_ws, void* stream);
+/* Chan-merge the per-block stats of the last gather(s) into d_stats =
+ * [n, mean[F], M2[F]] (fp64).  `n_parts` gathers may be accumulated: pass
+ * the workspace of each; merged in call order. */
+int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats,
+                          int accumulate, void* stream);
+
+/* ---- legacy MT19937 subsample indices (MxIF.py:484,490) ---------------------
+ * Bit-exact np.random.RandomState(seed).randint(0, high, size) (== choice),
+ * masked rejection on MT19937.  Host implementation (single thread). */
+int mw_legacy_randint_host(uint32_t seed, int64_t high, int64_t size, int32_t* h_out);
+
+/* ---- k-means++ (sklearn _kmeans.py:174-272) ---------------------------------
+ * Rows are scaled on the fly: x' = (x - mu) * inv_sigma  (fp64 affine).
+ * All state stays on device; no host synchronisation between steps. */
+size_t mw_kpp_ws_bytes(int64_t S, int T);
+int mw_kpp_init(const float* d_X, int64_t S, int F, const double* d_mu,
+                const double* d_inv, int64_t first, int T, void* d_ws, void* stream);
+/* one greedy step for center c (1..k-1); h_u = the T uniform draws */
+int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu,
+                const double* d_inv, int c, const double* h_u, int T,
+                void* d_ws, void* stream);
+/* chosen indices (int64 [k]) into d_idx_out */
+int mw_kpp_indices(const void* d_ws, int64_t S, int T, int k, int64_t* d_idx_out,
+                   void* stream);
+
+/* ---- Lloyd E(+M) step (sklearn _k_means_lloyd.pyx:23-218) -------------------
+ * Rows x' = x*scale_a[f] + scale_b[f] (fp32 affine, the folded StandardScaler).
+ * Labels argmin of the direct squared distance, lowest index on ties.
+ * mode 0: E+M (labels updated, changed count, per-cluster sums/counts)
+ * mode 1: E only + inertia (labels updated, sum of min distances)
+ * mode 2: inertia of the given labels only (fp64 distances)
+ * Per-block partial records [sums k*F | counts k | changed | inertia] go to
+ * d_ws; mw_lloyd_reduce folds them (fixed order) into d_out (fp64). */
+size_t mw_lloyd_ws_bytes(int64_t S, int k, int F);
+int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a,
+                  const float* d_b, const float* d_centers, int k,
+                  uint8_t* d_labels, int mode, void* d_ws, void* stream);
+int mw_lloyd_reduce(const void* d_ws, int64_t S, int k, int F, double* d_out,
+                    void* stream);
+
+/* ---- empty-cluster relocation support (_k_means_common.pyx:181-226) ---------
+ * fp64 distance of every row to centers[labels]; returns the n largest
+ * (value desc, index asc) into d_top_idx / d_top_val (n <= 64). */
+size_t mw_farthest_ws_bytes(int64_t S);
+int mw_farthest(const float* d_X, int64_t S, int F, const float* d_a,
+                const float* d_b, const double* d_centers, int k,
+                const uint8_t* d_labels, int n, int64_t* d_top_idx,
+                double* d_top_val, void* d_ws, void* stream);
+
+/* ---- label + confidence pass (MILWRM.py:237-277, 389-450) -------------------
+ * Over n_pix HWC fp32 pixels (C channels, features d_feat[F]):
+ * label = argmin_j ||x' - c_j||^2 (x' = x*a + b), conf = (d2 - d1)/d2;
+ * mask == 0 → label -1, conf NaN.  Per-block [sum conf | count] per label go
+ * to d_ws, mw_assign_reduce folds them into d_dom (fp64 [2k]). */
+size_t mw_assign_ws_bytes(int64_t n_pix, int k);
+int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F,
+                   const float* d_a, const float* d_b, const float* d_centers,
+                   int k, const uint8_t* d_mask, int64_t n_pix,
+                   int8_t* d_label, float* d_conf, void* d_ws, void* stream);
+int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom,
+                     void* stream);
+
+/* ---- synthetic slide generator (benchmark input; SURVEY §8d shape) ----------
+ * uint16 HWC + uint8 mask: Voronoi domains (seeds given), per-domain channel
+ * profiles, gamma-like multiplicative noise from a counter-based hash. */
+int mw_synth_slide(int H, int W, int C, const float* d_seed_yx, int n_seeds,
+                   const float* d_profiles, int n_domains, int shape_k,
+                   int bg_rows, uint64_t seed, uint16_t* d_img, uint8_t* d_mask,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MILWRM_AMD_H */

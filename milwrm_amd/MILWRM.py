@@ -1,0 +1,444 @@
+"""Tissue-domain labelers of MILWRM (MILWRM.py:29-2264) on the MI355X engine.
+
+Same classes, methods, arguments, attributes and error messages as the
+reference for the pixel-clustering path; the numerics behind them are the HIP
+kernels (fused lognorm+blur, subsample gather + column statistics, k-means++,
+fused Lloyd E+M, label+confidence pass).  Plotting / UMAP methods are outside
+the hot path and raise ``NotImplementedError``.
+
+Data placement: per-image pixels and the clustering rows stay in HBM; the
+reference's host attributes (``cluster_data``, ``tissue_IDs``,
+``confidence_IDs``) are materialised as float64 numpy arrays on first access.
+``n_jobs`` is accepted for signature compatibility and ignored (one process
+drives the device; multi-GPU runs go through ``milwrm_amd.dist``).
+"""
+from __future__ import annotations
+
+import itertools
+import os
+
+import numpy as np
+import pandas as pd
+import torch
+
+from . import device as D
+from .assign import assign_image, assign_rows, domain_means
+from .kmeans import DeviceRows, KMeans, StandardScaler
+from .MxIF import checktype, img
+from .ST import blur_features_st
+
+
+# ------------------------------------------------------------ k selection
+
+def kMeansRes(scaled_data, k, alpha_k=0.02, random_state=18):
+    """MILWRM.py:29-54: inertia / inertia_o + alpha_k * k."""
+    rows = scaled_data if isinstance(scaled_data, DeviceRows) else DeviceRows.from_host(scaled_data)
+    inertia_o = _inertia_o(rows)
+    kmeans = KMeans(n_clusters=k, random_state=random_state).fit(rows)
+    return kmeans.inertia_ / inertia_o + alpha_k * k
+
+
+def _inertia_o(rows: DeviceRows) -> float:
+    """sum((X - X.mean)^2) of the scaled rows = S * sum_f var_f."""
+    return float(rows.S * np.sum(rows.feature_var()))
+
+
+def chooseBestKforKMeansParallel(scaled_data, k_range, n_jobs=-1, **kwargs):
+    """MILWRM.py:57-90 (fits run one after another on the device)."""
+    rows = scaled_data if isinstance(scaled_data, DeviceRows) else DeviceRows.from_host(scaled_data)
+    ans = [kMeansRes(rows, k, **kwargs) for k in k_range]
+    ans = list(zip(k_range, ans))
+    results = pd.DataFrame(ans, columns=["k", "Scaled Inertia"]).set_index("k")
+    best_k = results.idxmin().iloc[0]
+    return best_k, results
+
+
+# --------------------------------------------------------- MxIF workers
+
+def prep_data_single_sample_mxif(image, use_path, mean, filter_name, sigma, features, fract,
+                                 path_save):
+    """MILWRM.py:172-234 (host-returning form)."""
+    if use_path:
+        if path_save is None:
+            raise Exception("Path to save final preprocessed npz files is requird when given path "
+                            "to image files")
+        image_path = image
+        image = img.from_npz(image_path + ".npz")
+    image.log_normalize(mean=mean)
+    image.blurring(filter_name=filter_name, sigma=sigma)
+    subsampled = image.subsample_pixels(features, fract)
+    if use_path:
+        file_save = _save_preprocessed(image, image_path, path_save)
+        return subsampled, file_save
+    return subsampled
+
+
+def _save_preprocessed(image, image_path, path_save):
+    new_image_path = os.path.join(path_save, "_final_preprocessed_images")
+    if not os.path.exists(new_image_path):
+        os.mkdir(new_image_path)
+    file_save = os.path.join(new_image_path, image_path.split("/")[-1] + "_final_preprocessed")
+    image.to_npz(file_save)
+    return file_save
+
+
+def add_tissue_ID_single_sample_mxif(image, use_path, features, kmeans, scaler):
+    """MILWRM.py:237-277: H x W float labels, NaN outside the mask."""
+    if use_path:
+        image = img.from_npz(image + ".npz")
+    lab, _, _ = _assign_img(image, features, kmeans.cluster_centers_, scaler)
+    return _labels_to_host(lab)
+
+
+def estimate_confidence_score_mxif(image, use_path, scaler, centroids, features, tissue_ID):
+    """MILWRM.py:389-450: (cID H x W float, NaN outside the mask; per-domain
+    mean over the given tissue_ID)."""
+    if use_path:
+        image = img.from_npz(image + ".npz")
+    lab, conf, dom = _assign_img(image, features, centroids, scaler)
+    cid = conf.double().cpu().numpy()
+    tid = np.asarray(tissue_ID)
+    own = _labels_to_host(lab)
+    if tid.shape == own.shape and np.array_equal(np.nan_to_num(tid, nan=-1), np.nan_to_num(own, nan=-1)):
+        means = domain_means(dom.cpu().numpy(), len(centroids))
+    else:
+        means = {}
+        with np.errstate(invalid="ignore"):
+            import warnings
+
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore", RuntimeWarning)
+                for i in range(len(centroids)):
+                    means[i] = np.mean(cid[tid == i])
+    return cid, means
+
+
+def estimate_confidence_score_st(sub_cluster_data, adata, centroids):
+    """MILWRM.py:557-598."""
+    _, cid, _ = assign_rows(sub_cluster_data, np.asarray(centroids, dtype=np.float64))
+    adata.obs["confidence_score"] = cid
+    score_df = pd.DataFrame(cid, columns=["score"])
+    score_df["tissue_ID"] = adata.obs["tissue_ID"].values
+    mean_conf_score = {}
+    for i in range(len(centroids)):
+        if (adata.obs["tissue_ID"] == i).any():
+            mean_conf_score[i] = score_df[score_df["tissue_ID"] == i]["score"].mean()
+        else:
+            mean_conf_score[i] = np.nan
+    return mean_conf_score
+
+
+def _assign_img(image: img, features, centers, scaler):
+    feats = image._features(features)
+    mu, inv = scaler.affine()
+    src = D.as_float32(image._materialize())
+    return assign_image(src, feats, mu, inv, np.asarray(centers, dtype=np.float64),
+                        image._mask_device())
+
+
+def _labels_to_host(lab: torch.Tensor) -> np.ndarray:
+    a = lab.cpu().numpy().astype(np.float64)
+    a[a < 0] = np.nan
+    return a
+
+
+class _LazyHostList(list):
+    """List of device tensors that reads as the reference's list of float64
+    host arrays (converted on first access, then cached)."""
+
+    def __init__(self, items, convert):
+        super().__init__(items)
+        self._convert = convert
+        self._done = [False] * len(items)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        if not self._done[i]:
+            super().__setitem__(i, self._convert(super().__getitem__(i)))
+            self._done[i] = True
+        return super().__getitem__(i)
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
+
+
+def _conf_to_host(conf: torch.Tensor) -> np.ndarray:
+    return conf.double().cpu().numpy()
+
+
+# ---------------------------------------------------------------- classes
+
+class tissue_labeler:
+    """MILWRM.py:647-922 (plots out of scope)."""
+
+    def __init__(self):
+        self._rows = None
+        self._cluster_host = None
+        self.k = None
+
+    # cluster_data: device rows, host float64 on read (MILWRM.py:1745)
+    @property
+    def cluster_data(self):
+        if self._cluster_host is None and self._rows is not None:
+            self._cluster_host = self._rows.to_host_scaled()
+        return self._cluster_host
+
+    @cluster_data.setter
+    def cluster_data(self, value):
+        self._rows = None
+        self._cluster_host = None if value is None else np.asarray(value, dtype=np.float64)
+
+    def _device_rows(self) -> DeviceRows:
+        if self._rows is None:
+            if self._cluster_host is None:
+                raise Exception("No cluster data found. Run prep_cluster_data() first.")
+            self._rows = DeviceRows.from_host(self._cluster_host)
+        return self._rows
+
+    def find_optimal_k(self, plot_out=False, alpha=0.05, random_state=18, n_jobs=-1):
+        """MILWRM.py:659-704: k in 2..20, best = first argmin of scaled inertia."""
+        if self._rows is None and self._cluster_host is None:
+            raise Exception("No cluster data found. Run prep_cluster_data() first.")
+        self.random_state = random_state
+        k_range = range(2, 21)
+        best_k, results = chooseBestKforKMeansParallel(self._device_rows(), k_range, n_jobs=n_jobs,
+                                                       random_state=random_state, alpha_k=alpha)
+        self.inertia_curve_ = results
+        print("The optimal number of clusters is {}".format(best_k))
+        self.k = int(best_k)
+
+    def find_tissue_regions(self, k=None, random_state=18):
+        """MILWRM.py:706-737."""
+        if self._rows is None and self._cluster_host is None:
+            raise Exception("No cluster data found. Run prep_cluster_data() first.")
+        if k is None and self.k is None:
+            raise Exception("No k found or provided. Run find_optimal_k() first or pass a k value.")
+        if k is not None:
+            print("Overriding optimal k value with k={}.".format(k))
+            self.k = k
+        self.random_state = random_state
+        print("Performing k-means clustering with {} target clusters".format(self.k))
+        self.kmeans = KMeans(n_clusters=self.k, random_state=random_state).fit(self._device_rows())
+
+    def _plot(self, *a, **k):
+        raise NotImplementedError("plotting is outside the MI355X hot path")
+
+    plot_feature_proportions = _plot
+    plot_feature_loadings = _plot
+    plot_percentage_variance_explained = _plot
+    plot_mse_mxif = _plot
+    plot_mse_st = _plot
+    plot_tissue_ID_proportions_mxif = _plot
+    plot_tissue_ID_proportions_st = _plot
+    make_umap = _plot
+    show_marker_overlay = _plot
+    plot_gene_loadings = _plot
+
+
+class mxif_labeler(tissue_labeler):
+    """MILWRM.py:1632-2264 (hot path)."""
+
+    def __init__(self, image_df):
+        tissue_labeler.__init__(self)
+        if np.all(image_df.columns == ["Img", "batch_names", "mean estimators", "pixels"]):
+            self.image_df = image_df
+        else:
+            raise Exception("Image_df must be given with these columns in this format ['Img', "
+                            "'batch_names', 'mean estimators', 'pixels']")
+        if self.image_df["Img"].apply(isinstance, args=[img]).all():
+            self.use_paths = False
+        elif self.image_df["Img"].apply(isinstance, args=[str]).all():
+            self.use_paths = True
+        else:
+            raise Exception("Img column in the dataframe should be either str for paths to the "
+                            "files or mxif.img object")
+
+    def _batch_means(self):
+        out = {}
+        for batch in self.image_df["batch_names"].unique():
+            sel = self.image_df[self.image_df["batch_names"] == batch]
+            est = sum(map(np.array, list(sel["mean estimators"])))
+            pixels = sum(sel["pixels"])
+            out[batch] = est / pixels
+        return out
+
+    def prep_cluster_data(self, features, filter_name="gaussian", sigma=2, fract=0.2,
+                          path_save=None):
+        """MILWRM.py:1672-1745: batch means, per-image lognorm + blur (one
+        fused kernel) + subsample gather straight into one HBM row block,
+        StandardScaler from device column statistics."""
+        if self._rows is not None or self._cluster_host is not None:
+            print("WARNING: overwriting existing cluster data")
+            self.cluster_data = None
+        self.model_features = features
+        use_path = self.use_paths
+        means = self._batch_means()
+        images = []
+        for image in self.image_df["Img"]:
+            if use_path:
+                if path_save is None:
+                    raise Exception("Path to save final preprocessed npz files is requird when "
+                                    "given path to image files")
+                images.append(img.from_npz(image + ".npz"))
+            else:
+                images.append(image)
+        # phase 1: mask ranks → sample counts → one preallocated row block
+        dev = D.device()
+        ranks = [D.mask_rank(im._mask_device().reshape(-1)) for im in images]
+        counts = [int(M * fract) for _, M in ranks]
+        F = len(images[0]._features(features))
+        X = torch.empty((sum(counts), F), dtype=torch.float32, device=dev)
+        stats = torch.zeros(1 + 2 * F, dtype=torch.float64, device=dev)
+        # phase 2: fused lognorm+blur, gather rows into X (image_df order)
+        off = 0
+        paths = []
+        for n_img, (im, batch, (r2p, M), S) in enumerate(
+                zip(images, self.image_df["batch_names"], ranks, counts)):
+            im.log_normalize(mean=means[batch])
+            im.blurring(filter_name=filter_name, sigma=sigma)
+            np.random.seed(16)
+            if S:
+                from .rng import subsample_indices
+
+                idx = subsample_indices(M, fract, 16)
+                feat = torch.as_tensor(np.asarray(im._features(features), dtype=np.int32), device=dev)
+                D.gather_rows(D.as_float32(im._device()), feat,
+                              torch.from_numpy(idx).to(dev, non_blocking=True), r2p,
+                              X[off:off + S], stats, accumulate=off > 0)
+            off += S
+            if use_path:
+                paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))
+        self.merged_batch_labels = list(itertools.chain(*[[x] * c for x, c in enumerate(counts)]))
+        if use_path:
+            self.image_df["Img"] = paths
+        else:
+            self._images = images
+        st = stats.cpu().numpy()
+        self.scaler = StandardScaler.from_stats(st)
+        mu, inv = self.scaler.affine()
+        self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv)
+        self._cluster_host = None
+
+    def _image_list(self):
+        if self.use_paths:
+            return [img.from_npz(p + ".npz") for p in self.image_df["Img"]]
+        return list(self.image_df["Img"])
+
+    def label_tissue_regions(self, k=None, alpha=0.05, plot_out=True, random_state=18, n_jobs=-1):
+        """MILWRM.py:1747-1794 plus the fused confidence pass (MILWRM.py:389-450
+        is computed in the same sweep over each image)."""
+        if k is None:
+            print("Determining optimal cluster number k via scaled inertia")
+            self.find_optimal_k(alpha=alpha, plot_out=plot_out, random_state=random_state,
+                                n_jobs=n_jobs)
+        self.find_tissue_regions(k=k, random_state=random_state)
+        print("Creating tissue_ID images for image objects...")
+        labs, confs, doms = [], [], []
+        for image in self._image_list():
+            lab, conf, dom = _assign_img(image, self.model_features, self.kmeans.cluster_centers_,
+                                         self.scaler)
+            labs.append(lab)
+            confs.append(conf)
+            doms.append(dom)
+        self._labels_dev, self._conf_dev, self._dom_dev = labs, confs, doms
+        self.tissue_IDs = _LazyHostList(labs, _labels_to_host)
+
+    def confidence_score_images(self):
+        """MILWRM.py:1868-1900 from the fused pass: confidence_IDs and the
+        images x domains DataFrame of mean confidences."""
+        k = self.kmeans.cluster_centers_.shape[0]
+        df = pd.DataFrame()
+        for i, dom in enumerate(self._dom_dev):
+            scores = domain_means(dom.cpu().numpy(), k)
+            d = pd.DataFrame(scores.values(), columns=[i])
+            df = pd.concat([df, d.T], ignore_index=True)
+        self.confidence_IDs = _LazyHostList(list(self._conf_dev), _conf_to_host)
+        self.confidence_score_df = df
+
+
+class st_labeler(tissue_labeler):
+    """MILWRM.py:925-1629 (ST plumbing; fit / confidence on the device)."""
+
+    def __init__(self, adatas):
+        tissue_labeler.__init__(self)
+        if not isinstance(adatas, list):
+            adatas = [adatas]
+        print("Initiating ST labeler with {} anndata objects".format(len(adatas)))
+        self.adatas = adatas
+        self.raw = adatas.copy()
+
+    def prep_cluster_data(self, use_rep, features=None, n_rings=1, histo=False,
+                          fluor_channels=None, spatial_graph_key=None, n_jobs=-1):
+        """MILWRM.py:951-1041."""
+        if self._rows is not None or self._cluster_host is not None:
+            print("WARNING: overwriting existing cluster data")
+            self.cluster_data = None
+        if features is None:
+            self.features = [x for x in range(self.adatas[0].obsm[use_rep].shape[1])]
+        else:
+            self.features = features
+        self.rep, self.histo, self.fluor_channels, self.n_rings = use_rep, histo, fluor_channels, n_rings
+        print("Collecting and blurring {} features from .obsm[{}]...".format(len(self.features), use_rep))
+        cluster_data = [prep_data_single_sample_st(a, i, use_rep, self.features, histo,
+                                                   fluor_channels, spatial_graph_key, n_rings)
+                        for i, a in enumerate(self.adatas)]
+        batch_labels = [[x] * len(cluster_data[x]) for x in range(len(cluster_data))]
+        self.merged_batch_labels = list(itertools.chain(*batch_labels))
+        subsampled_data = pd.concat(cluster_data)
+        self.scaler = StandardScaler().fit(subsampled_data.values)
+        self.cluster_data = self.scaler.transform(subsampled_data.values)
+        print("Collected clustering data of shape: {}".format(self.cluster_data.shape))
+
+    def label_tissue_regions(self, k=None, alpha=0.05, plot_out=True, random_state=18, n_jobs=-1):
+        """MILWRM.py:1043-1089 (labels are the fit labels, sliced per adata)."""
+        if k is None:
+            print("Determining optimal cluster number k via scaled inertia")
+            self.find_optimal_k(plot_out=plot_out, alpha=alpha, random_state=random_state,
+                                n_jobs=n_jobs)
+        self.find_tissue_regions(k=k, random_state=random_state)
+        start = 0
+        print("Adding tissue_ID label to anndata objects")
+        IDs = self.kmeans.labels_
+        for i in range(len(self.adatas)):
+            self.adatas[i].obs["tissue_ID"] = IDs[start:start + self.adatas[i].n_obs]
+            self.adatas[i].obs["tissue_ID"] = self.adatas[i].obs["tissue_ID"].astype("category")
+            self.adatas[i].obs["tissue_ID"] = self.adatas[i].obs["tissue_ID"].cat.set_categories(
+                np.unique(IDs))
+            start += self.adatas[i].n_obs
+
+    def confidence_score(self):
+        """MILWRM.py:1091-1121."""
+        assert self.kmeans is not None, "No cluster results found. Run label_tissue_regions() first."
+        i_slice = j_slice = 0
+        df_all = pd.DataFrame()
+        centroids = self.kmeans.cluster_centers_
+        for i, adata in enumerate(self.adatas):
+            j_slice += adata.n_obs
+            data = self.cluster_data[i_slice:j_slice]
+            scores = estimate_confidence_score_st(data, adata, centroids)
+            df = pd.DataFrame(scores.values(), columns=[i])
+            df_all = pd.concat([df_all, df], axis=1)
+            i_slice += adata.n_obs
+        self.confidence_score_df = df_all
+
+
+def prep_data_single_sample_st(adata, adata_i, use_rep, features, histo, fluor_channels,
+                               spatial_graph_key=None, n_rings=1):
+    """MILWRM.py:93-169."""
+    tmp = pd.DataFrame()
+    tmp[[use_rep + "_{}".format(x) for x in features]] = adata.obsm[use_rep][:, features]
+    if histo:
+        assert fluor_channels is None, "If histo is True, fluor_channels must be None. \
+            Histology specifies brightfield H&E with three (3) features."
+        print("Adding mean RGB histology features for adata #{}".format(adata_i))
+        tmp[["R_mean", "G_mean", "B_mean"]] = adata.obsm["image_means"]
+    if fluor_channels:
+        assert histo is False, "If fluorescence channels are given, histo must be False. \
+            Histology specifies brightfield H&E with three (3) features."
+        print("Adding mean fluorescent channels {} for adata #{}".format(fluor_channels, adata_i))
+        tmp[["ch_{}_mean".format(x) for x in fluor_channels]] = adata.obsm["image_means"][:, fluor_channels]
+    if n_rings > 0:
+        tmp = blur_features_st(adata, tmp, spatial_graph_key=spatial_graph_key, n_rings=n_rings)
+    return tmp

@@ -1,0 +1,111 @@
+"""ctypes binding of the milwrm_amd C ABI (include/milwrm_amd.h).
+
+``torch`` is imported first so that ``libmilwrm_amd.so`` binds to the HIP
+runtime already loaded by PyTorch (same soname ``libamdhip64.so.7``): device
+pointers and streams are then shared between the two.  There is no fallback:
+if the library is missing or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the library load: one HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmilwrm_amd.so")
+
+MW_U8, MW_U16, MW_F32 = 0, 1, 2
+_EINVAL, _EHIP, _EUNSUP = -1, -2, -3
+
+_lib = None
+_lock = threading.Lock()
+
+c_i64, c_i32, c_u32, c_u64 = C.c_int64, C.c_int, C.c_uint32, C.c_uint64
+c_f32, c_sz, c_vp = C.c_float, C.c_size_t, C.c_void_p
+c_dp = C.POINTER(C.c_double)
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "mw_version": (c_i32, []),
+    "mw_last_error": (C.c_char_p, []),
+    "mw_stream_blocks": (c_i32, [c_i64]),
+    "mw_nz_stats_ws_bytes": (c_sz, [c_i64, c_i32]),
+    "mw_nz_stats": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mw_lognorm": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_vp, c_f32, c_vp, c_vp]),
+    "mw_blur_ws_bytes": (c_sz, [c_i32, c_i32, c_i32, c_i32]),
+    "mw_blur": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_vp]),
+    "mw_block_mean": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "mw_mask_rank_ws_bytes": (c_sz, [c_i64]),
+    "mw_mask_rank": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "mw_gather_ws_bytes": (c_sz, [c_i64, c_i32]),
+    "mw_gather_rows": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "mw_col_stats_finalize": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),
+    "mw_legacy_randint_host": (c_i32, [c_u32, c_i64, c_i64, c_vp]),
+    "mw_kpp_ws_bytes": (c_sz, [c_i64, c_i32]),
+    "mw_kpp_init": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_kpp_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),
+    "mw_kpp_indices": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "mw_lloyd_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
+    "mw_lloyd_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),
+    "mw_lloyd_reduce": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "mw_farthest_ws_bytes": (c_sz, [c_i64]),
+    "mw_farthest": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mw_assign_ws_bytes": (c_sz, [c_i64, c_i32]),
+    "mw_assign_conf": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "mw_assign_reduce": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_synth_slide": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_u64, c_vp, c_vp, c_vp]),
+}
+
+EXPORTED = tuple(_PROTOS)
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the library; raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"milwrm_amd HIP library not found at {LIB_PATH}; build it with "
+                "`python -m milwrm_amd.build` (hipcc --offload-arch=gfx950)")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    return load().mw_last_error().decode(errors="replace")
+
+
+def check(status: int, what: str):
+    if status == 0:
+        return
+    msg = last_error()
+    if status == _EINVAL:
+        raise ValueError(f"{what}: {msg}")
+    if status == _EUNSUP:
+        raise NotImplementedError(f"{what}: {msg}")
+    raise NativeError(f"{what}: {msg} (status {status})")
+
+
+def call(name: str, *args):
+    """Invoke ``name`` and raise on a non-zero status."""
+    fn = getattr(load(), name)
+    check(fn(*args), name)
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))

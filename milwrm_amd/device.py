@@ -1,0 +1,190 @@
+"""Device engine: thin typed wrappers over the C ABI that take torch tensors
+(PyTorch supplies HBM allocations and the current HIP stream — plumbing only;
+every computation is a hand-written HIP kernel in ``csrc/``)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+_DTYPE_CODE = {torch.uint8: N.MW_U8, torch.int16: N.MW_U16, torch.float32: N.MW_F32}
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("milwrm_amd runs on an AMD Instinct GPU (HIP); no device is visible "
+                           "and there is no CPU fallback")
+    N.load()
+
+
+def device():
+    require_gpu()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def P(t):
+    """Raw device pointer of a tensor (or None)."""
+    return None if t is None else t.data_ptr()
+
+
+class Workspace:
+    """Grow-only scratch buffers per (device, tag); never freed inside a pass."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, tag: str, nbytes: int) -> torch.Tensor:
+        dev = torch.cuda.current_device()
+        key = (dev, tag)
+        b = self._bufs.get(key)
+        nbytes = max(int(nbytes), 256)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", dev))
+            self._bufs[key] = b
+        return b
+
+    def clear(self):
+        self._bufs.clear()
+
+
+WS = Workspace()
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _DTYPE_CODE[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported device image dtype {t.dtype}") from None
+
+
+def to_device_image(arr: np.ndarray) -> torch.Tensor:
+    """Upload an HWC host image keeping a compact element type: uint8/uint16
+    stay integral (uint16 travels as int16 bits), everything else → fp32."""
+    require_gpu()
+    a = np.ascontiguousarray(arr)
+    if a.dtype == np.uint8:
+        h = torch.from_numpy(a)
+    elif a.dtype == np.uint16:
+        h = torch.from_numpy(a.view(np.int16))
+    elif a.dtype == np.bool_:
+        h = torch.from_numpy(a.astype(np.uint8))
+    else:
+        if np.issubdtype(a.dtype, np.integer) and a.size and (a.min() >= 0 and a.max() <= 65535):
+            h = torch.from_numpy(a.astype(np.uint16).view(np.int16))
+        else:
+            h = torch.from_numpy(a.astype(np.float32))
+    return h.to(device(), non_blocking=False)
+
+
+def as_float32(t: torch.Tensor) -> torch.Tensor:
+    """Element-type cast of a raw device image (uint16 travels as int16)."""
+    if t.dtype == torch.float32:
+        return t
+    if t.dtype == torch.int16:
+        return (t.to(torch.int32) & 0xFFFF).to(torch.float32)
+    return t.to(torch.float32)
+
+
+def to_host_float64(t: torch.Tensor) -> np.ndarray:
+    if t.dtype == torch.int16:
+        return t.cpu().numpy().view(np.uint16).astype(np.float64)
+    return t.cpu().numpy().astype(np.float64)
+
+
+# ------------------------------------------------------------------ kernels
+
+def nz_stats(img: torch.Tensor):
+    """Per-channel (sum, count) of non-zero elements of an HWC image."""
+    H, W, C = img.shape
+    n_pix = H * W
+    s = torch.empty(C, dtype=torch.float64, device=img.device)
+    c = torch.empty(C, dtype=torch.int64, device=img.device)
+    ws = WS.get("nz", N.query("mw_nz_stats_ws_bytes", n_pix, C))
+    N.call("mw_nz_stats", P(img), dtype_code(img), n_pix, C, P(s), P(c), P(ws), stream())
+    return s, c
+
+
+def lognorm(img: torch.Tensor, inv_mean: torch.Tensor, pseudoval: float, out=None):
+    H, W, C = img.shape
+    if out is None:
+        out = torch.empty((H, W, C), dtype=torch.float32, device=img.device)
+    N.call("mw_lognorm", P(img), dtype_code(img), H * W, C, P(inv_mean), float(pseudoval),
+           P(out), stream())
+    return out
+
+
+def gaussian_taps(sigma: float, truncate: float = 4.0) -> np.ndarray:
+    """scipy ``_gaussian_kernel1d`` order 0 (radius int(truncate*sigma+0.5)),
+    computed in fp64 then rounded to fp32 for the kernel."""
+    r = int(truncate * float(sigma) + 0.5)
+    x = np.arange(-r, r + 1, dtype=np.float64)
+    phi = np.exp(-0.5 / (float(sigma) * float(sigma)) * x * x)
+    return (phi / phi.sum())[::-1].astype(np.float32).copy()  # correlate1d(weights[::-1])
+
+
+def blur(img: torch.Tensor, sigma: float, inv_mean=None, pseudoval: float = 1.0, out=None,
+         truncate: float = 4.0):
+    H, W, C = img.shape
+    w = gaussian_taps(sigma, truncate)
+    r = (len(w) - 1) // 2
+    if out is None:
+        out = torch.empty((H, W, C), dtype=torch.float32, device=img.device)
+    wsb = N.query("mw_blur_ws_bytes", H, W, C, r)
+    ws = WS.get("blur", wsb) if wsb else None
+    N.call("mw_blur", P(img), dtype_code(img), H, W, C, P(inv_mean), float(pseudoval),
+           w.ctypes.data, r, P(out), P(ws), stream())
+    return out
+
+
+def block_mean(img: torch.Tensor, fact: int):
+    H, W, C = img.shape
+    Ho, Wo = -(-H // fact), -(-W // fact)
+    out = torch.empty((Ho, Wo, C), dtype=torch.float32, device=img.device)
+    N.call("mw_block_mean", P(img), dtype_code(img), H, W, C, int(fact), P(out), stream())
+    return out
+
+
+def mask_rank(mask_u8: torch.Tensor):
+    """(rank→pixel uint32 tensor of length M, M) for mask != 0 (row-major)."""
+    n = mask_u8.numel()
+    r2p = torch.empty(n, dtype=torch.int32, device=mask_u8.device)
+    cnt = torch.empty(1, dtype=torch.int64, device=mask_u8.device)
+    ws = WS.get("mrank", N.query("mw_mask_rank_ws_bytes", n))
+    N.call("mw_mask_rank", P(mask_u8), n, P(r2p), P(cnt), P(ws), stream())
+    M = int(cnt.item())
+    return r2p[:M], M
+
+
+def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2p: torch.Tensor,
+                X_out: torch.Tensor, stats: torch.Tensor, accumulate: bool):
+    """X_out[j] = img[r2p[idx[j]], feat]; Chan-merge column stats into
+    ``stats`` = [n, mean[F], M2[F]] (fp64)."""
+    H, W, C = img_f32.shape
+    S, F = X_out.shape
+    if S == 0:
+        return
+    ws = WS.get("gather", N.query("mw_gather_ws_bytes", S, F))
+    N.call("mw_gather_rows", P(img_f32), C, P(feat), F, P(idx), P(r2p), S, P(X_out), P(ws), stream())
+    N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
+
+
+def synth_slide(H, W, C, seed, mode="hard", n_seeds=32, n_domains=8, bg_frac=0.15):
+    """Benchmark input generated on device (SURVEY §8d shape): uint16 HWC
+    (int16 storage) + uint8 mask."""
+    rng = np.random.default_rng(seed)
+    sp_, shape = (0.15, 1) if mode == "hard" else (0.8, 4)
+    syx = np.stack([rng.uniform(0, H, n_seeds), rng.uniform(0, W, n_seeds)], 1).astype(np.float32)
+    prof = rng.lognormal(4.0, sp_, size=(n_domains, C)).astype(np.float32)
+    dev = device()
+    d_syx = torch.from_numpy(syx.ravel()).to(dev)
+    d_prof = torch.from_numpy(prof.ravel()).to(dev)
+    img = torch.empty((H, W, C), dtype=torch.int16, device=dev)
+    mask = torch.empty((H, W), dtype=torch.uint8, device=dev)
+    N.call("mw_synth_slide", H, W, C, P(d_syx), n_seeds, P(d_prof), n_domains, shape,
+           int(round(bg_frac * H)), int(seed) & 0xFFFFFFFFFFFFFFFF, P(img), P(mask), stream())
+    return img, mask

@@ -1,0 +1,112 @@
+"""Host-side random-number plumbing that must reproduce NumPy's legacy
+``RandomState`` draws exactly (the reference seeds it: MxIF.py:484,
+MILWRM.py:52/735 → sklearn ``check_random_state``).
+
+* ``subsample_indices``: ``np.random.seed(16); np.random.choice(M, S)`` →
+  the library's bit-exact MT19937 masked-rejection generator (C, host).
+* ``kpp_draws``: the uniform doubles sklearn's ``_kmeans_plusplus`` consumes,
+  drawn up front (they do not depend on the data), so k-means++ runs on the
+  device with no host round trip.
+* ``first_center_index``: ``choice(n, p=ones/n)`` without materialising the
+  n-element cdf: the sequential fp64 running sum of 1/n advances by a constant
+  increment inside each binade (after one step), so it is evaluated run by run.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+def subsample_indices(M: int, fract: float, random_state: int = 16, out=None) -> np.ndarray:
+    """Indices of ``img.subsample_pixels`` (MxIF.py:484,490) as int32."""
+    from . import _native as N
+
+    S = int(M * fract)
+    if out is None:
+        out = np.empty(S, dtype=np.int32)
+    if S == 0:
+        return out[:0]
+    if M > 2**31:
+        raise NotImplementedError("subsample over more than 2^31 masked pixels")
+    N.call("mw_legacy_randint_host", int(random_state) & 0xFFFFFFFF, int(M), int(S),
+           out.ctypes.data)
+    return out
+
+
+def as_random_state(random_state):
+    """sklearn ``check_random_state`` semantics."""
+    if random_state is None or random_state is np.random:
+        return np.random.mtrand._rand
+    if isinstance(random_state, (int, np.integer)):
+        return np.random.RandomState(int(random_state))
+    if isinstance(random_state, np.random.RandomState):
+        return random_state
+    raise ValueError(f"{random_state!r} cannot be used to seed a RandomState instance")
+
+
+def kpp_draws(random_state, n_clusters: int, n_local_trials: int):
+    """(u0, [u_c for c in 1..k-1]) consumed by ``_kmeans_plusplus``
+    (_kmeans.py:225 choice → one random_sample; :243 uniform(size=T))."""
+    rs = as_random_state(random_state)
+    u0 = float(rs.random_sample())
+    steps = [rs.uniform(size=n_local_trials).astype(np.float64) for _ in range(1, n_clusters)]
+    return u0, steps
+
+
+def _runs(n: int):
+    """Yield (i0, s0, inc, m) runs: s_{i0+j} = s0 + j*inc for j in [0, m) where
+    s_i = fl(s_{i-1} + c), s_0 = c, c = 1/n (numpy sequential cumsum)."""
+    c = 1.0 / float(n)
+    i, s = 0, c
+    while i < n:
+        # one explicit step fixes the parity (round-half-even ties)
+        yield i, s, 0.0, 1
+        i += 1
+        if i >= n:
+            return
+        t = s + c
+        u = t + c
+        inc = u - t
+        m_exp = math.frexp(t)[1]  # t in [2^(m_exp-1), 2^m_exp)
+        top = math.ldexp(1.0, m_exp)
+        if inc > 0:
+            # largest j with t + j*inc < top, verified exactly below
+            j = int((top - t) / inc)
+            while j > 0 and t + float(j) * inc >= top:
+                j -= 1
+            while t + float(j + 1) * inc < top:
+                j += 1
+            m = min(j + 1, n - i)
+        else:
+            m = n - i
+        # the run t, t+inc, ..., holds while increments stay constant (same binade)
+        yield i, t, inc, m
+        i += m
+        s = (t + float(m - 1) * inc) + c  # s_i = fl(s_{i-1} + c)
+
+
+def _s_at(run, j):
+    i0, s0, inc, m = run
+    return s0 + float(j) * inc
+
+
+def first_center_index(n: int, u: float) -> int:
+    """``RandomState.choice(n, p=ones(n)/n)`` given its uniform draw ``u``."""
+    if n <= 0:
+        raise ValueError("n must be positive")
+    runs = list(_runs(n))
+    last = runs[-1]
+    total = _s_at(last, last[3] - 1)
+    for run in runs:
+        i0, s0, inc, m = run
+        if _s_at(run, m - 1) / total > u:
+            lo, hi = 0, m - 1  # first j with s_j/total > u
+            while lo < hi:
+                mid = (lo + hi) // 2
+                if _s_at(run, mid) / total > u:
+                    hi = mid
+                else:
+                    lo = mid + 1
+            return i0 + lo
+    return n  # u >= 1 is impossible for random_sample; numpy would return n

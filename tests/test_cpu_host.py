@@ -1,0 +1,115 @@
+"""CPU-only tests: the C-ABI library loads and exports every declared symbol,
+the host-side RNG plumbing is bit-exact with NumPy, and the host API checks
+behave like the reference's (no compute calls — no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from tests.conftest import ROOT
+
+
+def _declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "milwrm_amd.h")).read()
+    return sorted(set(re.findall(r"\b(mw_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_all_header_symbols():
+    from milwrm_amd import _native as N
+
+    lib = N.load()
+    syms = _declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), f"missing export {s}"
+    assert set(syms) == set(N.EXPORTED), "ctypes prototypes out of sync with include/milwrm_amd.h"
+    assert lib.mw_version() >= 10000
+
+
+def test_legacy_randint_host_bit_exact():
+    from milwrm_amd.rng import subsample_indices
+
+    for M, fr in [(6540, 0.2), (1, 0.9), (2, 0.5), (1000, 0.5), (2**20, 0.01), (2**20 + 1, 0.01),
+                  (123457, 0.3), (2**31 - 1, 1e-6), (85_000_000, 0.001)]:
+        np.random.seed(16)
+        ref = np.random.choice(M, int(M * fr))
+        got = subsample_indices(M, fr, 16)
+        np.testing.assert_array_equal(got, ref, err_msg=f"M={M}")
+
+
+def test_first_center_index_matches_numpy_choice():
+    from milwrm_amd.rng import first_center_index, kpp_draws
+
+    for n in (1, 2, 3, 5, 17, 6297, 65537, 100003, 999999, 2**20 + 7):
+        for seed in (18, 0, 12345):
+            ref = np.random.RandomState(seed).choice(n, p=np.ones(n) / n)
+            u0, _ = kpp_draws(seed, 2, 2)
+            assert first_center_index(n, u0) == ref, (n, seed)
+
+
+def test_kpp_draws_consume_like_sklearn():
+    from milwrm_amd.rng import kpp_draws
+
+    rs = np.random.RandomState(18)
+    u0 = rs.random_sample()
+    steps = [rs.uniform(size=4) for _ in range(7)]
+    a0, a = kpp_draws(18, 8, 4)
+    assert a0 == u0
+    for x, y in zip(a, steps):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_gaussian_taps_match_scipy():
+    import scipy.ndimage as ndi
+
+    from milwrm_amd.device import gaussian_taps
+
+    for s in (0.5, 1.0, 2.0, 3.7):
+        w = gaussian_taps(s)
+        imp = np.zeros(101)
+        imp[50] = 1.0
+        ref = ndi.gaussian_filter1d(imp, s, mode="nearest", truncate=4.0)
+        r = (len(w) - 1) // 2
+        np.testing.assert_allclose(w[::-1], ref[50 - r:50 + r + 1], rtol=1e-6)
+
+
+def test_img_and_labeler_validation_like_reference():
+    import milwrm_amd as M
+
+    with pytest.raises(AssertionError, match="enough dimensions"):
+        M.img(np.zeros(5))
+    with pytest.raises(Exception, match="Channels must be given in a list"):
+        M.img(np.zeros((4, 4, 2)), channels=("a", "b"))
+    with pytest.raises(AssertionError, match="Shape of mask"):
+        M.img(np.zeros((4, 4, 2)), mask=np.ones((3, 4)))
+    im = M.img(np.zeros((4, 4, 2)))
+    assert im.ch == ["ch_0", "ch_1"] and im.n_ch == 2
+    with pytest.raises(Exception, match="Image_df must be given"):
+        M.mxif_labeler(pd.DataFrame({"Img": [im], "batch": ["a"], "mean": [[1]], "pixels": [1]}))
+    df = pd.DataFrame({"Img": [im, "p"], "batch_names": ["a", "a"], "mean estimators": [[1], [1]],
+                       "pixels": [1, 1]})
+    with pytest.raises(Exception, match="Img column"):
+        M.mxif_labeler(df)
+    lab = M.mxif_labeler(df.iloc[:1])
+    with pytest.raises(Exception, match="No cluster data found"):
+        lab.find_optimal_k()
+    with pytest.raises(Exception, match="No cluster data found"):
+        lab.find_tissue_regions(k=3)
+    with pytest.raises(Exception, match="filter name should be"):
+        im.blurring("nope")
+    with pytest.raises(TypeError):
+        im.blurring("median", sigma=2)  # the reference's median branch raises (MxIF.py:403)
+
+
+def test_scaler_constant_feature_rule():
+    from milwrm_amd.kmeans import StandardScaler
+
+    X = np.column_stack([np.arange(10.0), np.full(10, 3.0)])
+    s = StandardScaler().fit(X)
+    assert s.scale_[1] == 1.0
+    st = np.concatenate([[10.0], X.mean(0), X.var(0) * 10])
+    s2 = StandardScaler.from_stats(st)
+    np.testing.assert_allclose(s2.scale_, s.scale_)
