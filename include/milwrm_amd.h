@@ -114,17 +114,36 @@ int mw_legacy_randint_host(uint32_t seed, int64_t high, int64_t size, int32_t* h
 
 /* ---- k-means++ (sklearn _kmeans.py:174-272) ---------------------------------
  * Rows are scaled on the fly: x' = (x - mu) * inv_sigma  (fp64 affine).
- * All state stays on device; no host synchronisation between steps. */
+ * Single device: mw_kpp_init + (k-1) x mw_kpp_step + mw_kpp_indices keep all
+ * state on the device (no host synchronisation between steps).
+ * Row-sharded (one shard per rank): mw_kpp_init, then per step c
+ * mw_kpp_pots → (host all-gather, global argmin, targets) → mw_kpp_search
+ * with explicit local targets → (host all-reduce of candidate rows) →
+ * mw_kpp_trial. */
 size_t mw_kpp_ws_bytes(int64_t S, int T);
+/* distances to one center row (raw fp32 features, device) */
 int mw_kpp_init(const float* d_X, int64_t S, int F, const double* d_mu,
-                const double* d_inv, int64_t first, int T, void* d_ws, void* stream);
-/* one greedy step for center c (1..k-1); h_u = the T uniform draws */
+                const double* d_inv, const float* d_center_row, int T, void* d_ws,
+                void* stream);
+/* single-device step for center c (1..k-1); h_u = the T uniform draws */
 int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu,
                 const double* d_inv, int c, const double* h_u, int T,
                 void* d_ws, void* stream);
-/* chosen indices (int64 [k]) into d_idx_out */
+/* single-device: chosen indices (int64 [k]) into d_idx_out */
 int mw_kpp_indices(const void* d_ws, int64_t S, int T, int k, int64_t* d_idx_out,
                    void* stream);
+/* sharded: local potentials (fp64) of the arrays finished before step c
+ * (1 array after init, T after a trial) */
+int mw_kpp_pots(const void* d_ws, int64_t S, int T, int c, double* d_pots, void* stream);
+/* sharded: search array `best` of step c-1 for local targets d_rv[T] (fp64,
+ * < 0 = not on this shard); local row indices (int64, -1 if skipped) */
+int mw_kpp_search(void* d_ws, int64_t S, int T, int c, int best, const double* d_rv,
+                  int64_t* d_local_idx, void* stream);
+/* sharded: trial pass of step c against candidate rows d_rows (T x F raw
+ * fp32), minimum taken with array `best` of step c-1 */
+int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu,
+                 const double* d_inv, int c, int best, const float* d_rows, int T,
+                 void* d_ws, void* stream);
 
 /* ---- Lloyd E(+M) step (sklearn _k_means_lloyd.pyx:23-218) -------------------
  * Rows x' = x*scale_a[f] + scale_b[f] (fp32 affine, the folded StandardScaler).

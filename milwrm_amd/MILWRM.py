@@ -26,27 +26,32 @@ from .assign import assign_image, assign_rows, domain_means
 from .kmeans import DeviceRows, KMeans, StandardScaler
 from .MxIF import checktype, img
 from .ST import blur_features_st
+from .dist import LOCAL_COMM
 
 
 # ------------------------------------------------------------ k selection
 
-def kMeansRes(scaled_data, k, alpha_k=0.02, random_state=18):
+def kMeansRes(scaled_data, k, alpha_k=0.02, random_state=18, comm=None):
     """MILWRM.py:29-54: inertia / inertia_o + alpha_k * k."""
+    comm = LOCAL_COMM if comm is None else comm
     rows = scaled_data if isinstance(scaled_data, DeviceRows) else DeviceRows.from_host(scaled_data)
-    inertia_o = _inertia_o(rows)
-    kmeans = KMeans(n_clusters=k, random_state=random_state).fit(rows)
+    inertia_o = _inertia_o(rows, comm)
+    kmeans = KMeans(n_clusters=k, random_state=random_state).fit(rows, comm=comm)
     return kmeans.inertia_ / inertia_o + alpha_k * k
 
 
-def _inertia_o(rows: DeviceRows) -> float:
-    """sum((X - X.mean)^2) of the scaled rows = S * sum_f var_f."""
-    return float(rows.S * np.sum(rows.feature_var()))
+def _inertia_o(rows: DeviceRows, comm=LOCAL_COMM) -> float:
+    """sum((X - X.mean)^2) of the scaled rows = S_total * sum_f var_f."""
+    S = rows.S
+    if comm.sharded():
+        S = int(comm.all_gather_np(np.array([S], dtype=np.int64))[:, 0].sum())
+    return float(S * np.sum(rows.feature_var()))
 
 
-def chooseBestKforKMeansParallel(scaled_data, k_range, n_jobs=-1, **kwargs):
+def chooseBestKforKMeansParallel(scaled_data, k_range, n_jobs=-1, comm=None, **kwargs):
     """MILWRM.py:57-90 (fits run one after another on the device)."""
     rows = scaled_data if isinstance(scaled_data, DeviceRows) else DeviceRows.from_host(scaled_data)
-    ans = [kMeansRes(rows, k, **kwargs) for k in k_range]
+    ans = [kMeansRes(rows, k, comm=comm, **kwargs) for k in k_range]
     ans = list(zip(k_range, ans))
     results = pd.DataFrame(ans, columns=["k", "Scaled Inertia"]).set_index("k")
     best_k = results.idxmin().iloc[0]
@@ -177,6 +182,7 @@ class tissue_labeler:
         self._rows = None
         self._cluster_host = None
         self.k = None
+        self._comm = LOCAL_COMM
 
     # cluster_data: device rows, host float64 on read (MILWRM.py:1745)
     @property
@@ -204,7 +210,8 @@ class tissue_labeler:
         self.random_state = random_state
         k_range = range(2, 21)
         best_k, results = chooseBestKforKMeansParallel(self._device_rows(), k_range, n_jobs=n_jobs,
-                                                       random_state=random_state, alpha_k=alpha)
+                                                       comm=self._comm, random_state=random_state,
+                                                       alpha_k=alpha)
         self.inertia_curve_ = results
         print("The optimal number of clusters is {}".format(best_k))
         self.k = int(best_k)
@@ -220,7 +227,8 @@ class tissue_labeler:
             self.k = k
         self.random_state = random_state
         print("Performing k-means clustering with {} target clusters".format(self.k))
-        self.kmeans = KMeans(n_clusters=self.k, random_state=random_state).fit(self._device_rows())
+        self.kmeans = KMeans(n_clusters=self.k, random_state=random_state).fit(
+            self._device_rows(), comm=self._comm)
 
     def _plot(self, *a, **k):
         raise NotImplementedError("plotting is outside the MI355X hot path")
@@ -255,26 +263,31 @@ class mxif_labeler(tissue_labeler):
             raise Exception("Img column in the dataframe should be either str for paths to the "
                             "files or mxif.img object")
 
-    def _batch_means(self):
-        out = {}
+    def _batch_means(self, comm=LOCAL_COMM):
+        """MILWRM.py:1706-1714 (summed over ranks when sharded)."""
+        per = {}
         for batch in self.image_df["batch_names"].unique():
             sel = self.image_df[self.image_df["batch_names"] == batch]
-            est = sum(map(np.array, list(sel["mean estimators"])))
-            pixels = sum(sel["pixels"])
-            out[batch] = est / pixels
-        return out
+            per[batch] = (sum(map(np.array, list(sel["mean estimators"]))), sum(sel["pixels"]))
+        if comm.sharded():
+            per = comm.sum_batches(per)
+        return {b: est / pixels for b, (est, pixels) in per.items()}
 
     def prep_cluster_data(self, features, filter_name="gaussian", sigma=2, fract=0.2,
-                          path_save=None):
+                          path_save=None, comm=None):
         """MILWRM.py:1672-1745: batch means, per-image lognorm + blur (one
         fused kernel) + subsample gather straight into one HBM row block,
-        StandardScaler from device column statistics."""
+        StandardScaler from device column statistics.  With a sharded
+        ``comm`` (milwrm_amd.dist) each rank holds its own slides and the
+        statistics are merged across ranks."""
+        comm = LOCAL_COMM if comm is None else comm
+        self._comm = comm
         if self._rows is not None or self._cluster_host is not None:
             print("WARNING: overwriting existing cluster data")
             self.cluster_data = None
         self.model_features = features
         use_path = self.use_paths
-        means = self._batch_means()
+        means = self._batch_means(comm)
         images = []
         for image in self.image_df["Img"]:
             if use_path:
@@ -315,7 +328,7 @@ class mxif_labeler(tissue_labeler):
             self.image_df["Img"] = paths
         else:
             self._images = images
-        st = stats.cpu().numpy()
+        st = comm.merge_stats(stats.cpu().numpy(), F)
         self.scaler = StandardScaler.from_stats(st)
         mu, inv = self.scaler.affine()
         self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv)
@@ -326,9 +339,12 @@ class mxif_labeler(tissue_labeler):
             return [img.from_npz(p + ".npz") for p in self.image_df["Img"]]
         return list(self.image_df["Img"])
 
-    def label_tissue_regions(self, k=None, alpha=0.05, plot_out=True, random_state=18, n_jobs=-1):
+    def label_tissue_regions(self, k=None, alpha=0.05, plot_out=True, random_state=18, n_jobs=-1,
+                             comm=None):
         """MILWRM.py:1747-1794 plus the fused confidence pass (MILWRM.py:389-450
         is computed in the same sweep over each image)."""
+        if comm is not None:
+            self._comm = comm
         if k is None:
             print("Determining optimal cluster number k via scaled inertia")
             self.find_optimal_k(alpha=alpha, plot_out=plot_out, random_state=random_state,

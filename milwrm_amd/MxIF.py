@@ -37,6 +37,22 @@ scale_rgb = _out_of_scope("scale_rgb")
 CLAHE = _out_of_scope("CLAHE")
 
 
+class _DeviceMask:
+    """Host-side stand-in for a mask that lives in HBM (materialised on use)."""
+
+    def __init__(self, t):
+        self._t = t
+        self.shape = tuple(t.shape)
+        self.dtype = np.dtype(np.uint8)
+
+    def __array__(self, dtype=None, copy=None):
+        a = self._t.cpu().numpy()
+        return a if dtype is None else a.astype(dtype)
+
+    def copy(self):
+        return _DeviceMask(self._t.clone())
+
+
 class img:
     def __init__(self, img_arr, channels=None, mask=None):
         """Same validation and attributes as MxIF.py:126-167 (``img``, ``n_ch``,
@@ -164,6 +180,26 @@ class img:
 
     def __getitem__(self, channels):
         return self.img[:, :, self._features(channels)]
+
+    @classmethod
+    def from_device(cls, tensor, mask=None, channels=None) -> "img":
+        """Wrap an HWC image already resident in HBM (uint8 / uint16-as-int16 /
+        fp32) and an optional device mask (nonzero = tissue)."""
+        assert tensor.dim() == 3, "device image must be H x W x C"
+        obj = cls.__new__(cls)
+        obj._ndim = 3
+        obj._host = None
+        obj._host64 = None
+        obj._dev = tensor
+        obj._pending = None
+        obj.n_ch = int(tensor.shape[2])
+        obj.ch = channels if channels is not None else ["ch_{}".format(x) for x in range(obj.n_ch)]
+        obj._mask = None
+        obj._mask_dev = None
+        if mask is not None:
+            obj._mask = _DeviceMask(mask)
+            obj._mask_dev = (mask != 0).to(torch.uint8) if mask.dtype != torch.uint8 else mask
+        return obj
 
     # ----------------------------------------------------------------- I/O
     @classmethod

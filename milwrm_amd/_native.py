@@ -44,9 +44,12 @@ _PROTOS = {
     "mw_col_stats_finalize": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),
     "mw_legacy_randint_host": (c_i32, [c_u32, c_i64, c_i64, c_vp]),
     "mw_kpp_ws_bytes": (c_sz, [c_i64, c_i32]),
-    "mw_kpp_init": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_kpp_init": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "mw_kpp_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_kpp_indices": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "mw_kpp_pots": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "mw_kpp_search": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "mw_kpp_trial": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_lloyd_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "mw_lloyd_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_lloyd_reduce": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),

@@ -7,6 +7,7 @@ import torch
 
 from . import _native as N
 from . import device as D
+from . import profiling
 
 
 def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
@@ -30,8 +31,9 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
     dom = torch.empty(2 * k, dtype=torch.float64, device=dev)
     ws = D.WS.get("assign", N.query("mw_assign_ws_bytes", n, k))
     st = D.stream()
-    N.call("mw_assign_conf", D.P(img_f32), C, D.P(feat), F, D.P(a), D.P(b), D.P(c32), k,
-           D.P(mask_u8), n, D.P(lab), D.P(conf), D.P(ws), st)
+    with profiling.timed("assign_conf", n * (C * 4 + 1 + 5)):
+        N.call("mw_assign_conf", D.P(img_f32), C, D.P(feat), F, D.P(a), D.P(b), D.P(c32), k,
+               D.P(mask_u8), n, D.P(lab), D.P(conf), D.P(ws), st)
     N.call("mw_assign_reduce", D.P(ws), n, k, D.P(dom), st)
     return lab, conf, dom
 

@@ -74,10 +74,11 @@ __device__ __host__ inline KppState kpp_state(char* base, const KppLayout& L, in
 }
 
 // distance of every row to one center row (fp64), block sums.  Writes
-// bank[0][0][:] and bsum[0][0][:]; chosen[0] = first.
+// bank[0][0][:] and bsum[0][0][:].
 __global__ void __launch_bounds__(256) kpp_init_kernel(const float* __restrict__ X, int64_t S, int F,
                                                        const double* __restrict__ mu,
-                                                       const double* __restrict__ inv, int64_t first,
+                                                       const double* __restrict__ inv,
+                                                       const float* __restrict__ crow,
                                                        int64_t R, double* __restrict__ out,
                                                        double* __restrict__ bsum,
                                                        int64_t* __restrict__ chosen) {
@@ -85,8 +86,8 @@ __global__ void __launch_bounds__(256) kpp_init_kernel(const float* __restrict__
   __shared__ double s_c[256];
   __shared__ double s_red[4];
   const int t = threadIdx.x;
-  for (int f = t; f < F; f += 256) s_c[f] = ((double)X[first * F + f] - mu[f]) * inv[f];
-  if (blockIdx.x == 0 && t == 0) chosen[0] = first;
+  for (int f = t; f < F; f += 256) s_c[f] = ((double)crow[f] - mu[f]) * inv[f];
+  if (blockIdx.x == 0 && t == 0) chosen[0] = -1;  // the caller knows the first index
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
   double acc = 0.0;
   __syncthreads();
@@ -123,6 +124,17 @@ __device__ __forceinline__ void scan_blocks(const double* __restrict__ bs, int G
   }
 }
 
+// local potentials of the n_cur arrays (same scan order as the search)
+__global__ void __launch_bounds__(1024) kpp_pots_kernel(const double* __restrict__ bsum_cur,
+                                                        int n_cur, int G, double* __restrict__ pots) {
+  __shared__ double s[1024];
+  for (int i = 0; i < n_cur; ++i) {
+    scan_blocks(bsum_cur + (size_t)i * G, G, s);
+    if (threadIdx.x == 0) pots[i] = s[G - 1];
+    __syncthreads();
+  }
+}
+
 // select best candidate of the finished step (argmin of potentials, first
 // wins), then draw the next step's candidates: targets u_t * pot, located by
 // the block prefix then a chunked scan inside the block.
@@ -135,28 +147,36 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(const double* __restri
                                                           double u5, double u6, double u7, int T,
                                                           int64_t* __restrict__ cand,
                                                           int64_t* __restrict__ chosen,
-                                                          int* __restrict__ best_out) {
+                                                          int* __restrict__ best_out,
+                                                          int best_given,
+                                                          const double* __restrict__ rv_given) {
   __shared__ double s[1024];
   __shared__ double s_pot[8];
   __shared__ int s_best;
   __shared__ double s_chunk[1024];
   __shared__ int s_found;
   const int t = threadIdx.x;
-  // 1) potentials of the n_cur arrays of the finished step → best
-  for (int i = 0; i < n_cur; ++i) {
-    scan_blocks(bsum_cur + (size_t)i * G, G, s);
-    if (t == 0) s_pot[i] = s[G - 1];
+  if (best_given >= 0) {
+    // sharded mode: the host chose the global best
+    if (t == 0) { s_best = best_given; *best_out = best_given; }
+    __syncthreads();
+  } else {
+    // 1) potentials of the n_cur arrays of the finished step → best
+    for (int i = 0; i < n_cur; ++i) {
+      scan_blocks(bsum_cur + (size_t)i * G, G, s);
+      if (t == 0) s_pot[i] = s[G - 1];
+      __syncthreads();
+    }
+    if (t == 0) {
+      int b = 0;
+      for (int i = 1; i < n_cur; ++i)
+        if (s_pot[i] < s_pot[b]) b = i;
+      s_best = b;
+      *best_out = b;
+      if (c_done > 0) chosen[c_done] = cand[b];
+    }
     __syncthreads();
   }
-  if (t == 0) {
-    int b = 0;
-    for (int i = 1; i < n_cur; ++i)
-      if (s_pot[i] < s_pot[b]) b = i;
-    s_best = b;
-    *best_out = b;
-    if (c_done > 0) chosen[c_done] = cand[b];
-  }
-  __syncthreads();
   const int b = s_best;
   if (T == 0) return;  // final selection only
   const double* d = bank_cur + (size_t)b * S;
@@ -164,7 +184,11 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(const double* __restri
   const double pot = s[G - 1];
   const double us[8] = {u0, u1, u2, u3, u4, u5, u6, u7};
   for (int k = 0; k < T; ++k) {
-    const double rv = us[k] * pot;
+    const double rv = rv_given ? rv_given[k] : us[k] * pot;
+    if (rv < 0.0) {  // target not on this shard
+      if (t == 0) cand[k] = -1;
+      continue;      // uniform: every thread reads the same rv
+    }
     // first block whose inclusive prefix reaches rv (else the last block)
     if (t == 0) s_found = G - 1;
     __syncthreads();
@@ -215,8 +239,9 @@ __global__ void __launch_bounds__(256) kpp_trial_kernel(const float* __restrict_
                                                         const double* __restrict__ mu,
                                                         const double* __restrict__ inv,
                                                         const double* __restrict__ bank_prev,
-                                                        const int* __restrict__ best,
-                                                        const int64_t* __restrict__ cand, int T,
+                                                        const int* __restrict__ best, int best_val,
+                                                        const int64_t* __restrict__ cand,
+                                                        const float* __restrict__ cand_rows, int T,
                                                         int64_t R, double* __restrict__ bank_new,
                                                         double* __restrict__ bsum_new) {
   extern __shared__ __attribute__((aligned(16))) float s_tile[];
@@ -225,9 +250,10 @@ __global__ void __launch_bounds__(256) kpp_trial_kernel(const float* __restrict_
   const int t = threadIdx.x;
   for (int q = t; q < T * F; q += 256) {
     const int k = q / F, f = q - k * F;
-    s_c[k * 64 + f] = ((double)X[cand[k] * F + f] - mu[f]) * inv[f];
+    const float xv = cand_rows ? cand_rows[k * F + f] : X[cand[k] * F + f];
+    s_c[k * 64 + f] = ((double)xv - mu[f]) * inv[f];
   }
-  const double* cur = bank_prev + (size_t)(*best) * S;
+  const double* cur = bank_prev + (size_t)(best ? *best : best_val) * S;
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
   double acc[8];
 #pragma unroll
@@ -612,20 +638,32 @@ extern "C" {
 
 size_t mw_kpp_ws_bytes(int64_t S, int T) { return kpp_layout(S, T).total; }
 
+struct KppPtrs {
+  KppLayout L;
+  KppState st;
+  double *bank, *bsum;
+  double* bank_of(int c, int T, int64_t S) const { return bank + (size_t)(c & 1) * T * S; }
+  double* bsum_of(int c, int T) const { return bsum + (size_t)(c & 1) * T * L.G; }
+};
+static KppPtrs kpp_ptrs(const void* d_ws, int64_t S, int T) {
+  KppPtrs p;
+  p.L = kpp_layout(S, T);
+  char* base = reinterpret_cast<char*>(const_cast<void*>(d_ws));
+  p.st = kpp_state(base, p.L, T);
+  p.bank = reinterpret_cast<double*>(base + p.L.bank);
+  p.bsum = reinterpret_cast<double*>(base + p.L.bsum);
+  return p;
+}
+
 int mw_kpp_init(const float* d_X, int64_t S, int F, const double* d_mu, const double* d_inv,
-                int64_t first, int T, void* d_ws, void* stream) {
-  MW_CHECK_ARG(d_X && d_mu && d_inv && d_ws, "mw_kpp_init: null pointer");
+                const float* d_center_row, int T, void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_X && d_mu && d_inv && d_ws && d_center_row, "mw_kpp_init: null pointer");
   MW_CHECK_ARG(S > 0 && F > 0 && F <= 256, "mw_kpp_init: bad shape");
   MW_CHECK_ARG(T >= 1 && T <= 8, "mw_kpp_init: n_local_trials must be in [1, 8]");
-  MW_CHECK_ARG(first >= 0 && first < S, "mw_kpp_init: first index out of range");
-  const KppLayout L = kpp_layout(S, T);
-  char* base = reinterpret_cast<char*>(d_ws);
-  KppState st = kpp_state(base, L, T);
-  double* bank0 = reinterpret_cast<double*>(base + L.bank);
-  double* bsum0 = reinterpret_cast<double*>(base + L.bsum);
-  hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(kpp_init_kernel, dim3(L.G), dim3(256), (size_t)kT * F * sizeof(float), s, d_X,
-                     S, F, d_mu, d_inv, first, krows(S), bank0, bsum0, st.chosen);
+  const KppPtrs p = kpp_ptrs(d_ws, S, T);
+  hipLaunchKernelGGL(kpp_init_kernel, dim3(p.L.G), dim3(256), (size_t)kT * F * sizeof(float),
+                     as_stream(stream), d_X, S, F, d_mu, d_inv, d_center_row, krows(S),
+                     p.bank_of(0, T, S), p.bsum_of(0, T), p.st.chosen);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
@@ -635,49 +673,75 @@ int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu, const do
   MW_CHECK_ARG(d_X && d_mu && d_inv && d_ws && h_u, "mw_kpp_step: null pointer");
   MW_CHECK_ARG(c >= 1 && c < 256, "mw_kpp_step: center index %d out of range", c);
   MW_CHECK_ARG(T >= 1 && T <= 8 && F <= 64, "mw_kpp_step: T in [1,8], F <= 64 required");
-  const KppLayout L = kpp_layout(S, T);
-  char* base = reinterpret_cast<char*>(d_ws);
-  KppState st = kpp_state(base, L, T);
-  double* bank = reinterpret_cast<double*>(base + L.bank);
-  double* bsum = reinterpret_cast<double*>(base + L.bsum);
-  const int prev = (c - 1) & 1, next = c & 1;
-  double* bank_prev = bank + (size_t)prev * T * S;
-  double* bsum_prev = bsum + (size_t)prev * T * L.G;
-  double* bank_next = bank + (size_t)next * T * S;
-  double* bsum_next = bsum + (size_t)next * T * L.G;
+  const KppPtrs p = kpp_ptrs(d_ws, S, T);
   const int n_cur = c == 1 ? 1 : T;
   double u[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = 0; i < T; ++i) u[i] = h_u[i];
   hipStream_t s = as_stream(stream);
   // select the previous step's best (c >= 2), then locate this step's candidates
-  hipLaunchKernelGGL(kpp_search_kernel, dim3(1), dim3(1024), 0, s, bank_prev, bsum_prev, n_cur, S,
-                     L.G, krows(S), c - 1, u[0], u[1], u[2], u[3], u[4], u[5], u[6], u[7], T,
-                     st.cand, st.chosen, st.best);
+  hipLaunchKernelGGL(kpp_search_kernel, dim3(1), dim3(1024), 0, s, p.bank_of(c - 1, T, S),
+                     p.bsum_of(c - 1, T), n_cur, S, p.L.G, krows(S), c - 1, u[0], u[1], u[2], u[3],
+                     u[4], u[5], u[6], u[7], T, p.st.cand, p.st.chosen, p.st.best, -1,
+                     (const double*)nullptr);
   MW_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kpp_trial_kernel, dim3(L.G), dim3(256), (size_t)kT * F * sizeof(float), s, d_X,
-                     S, F, d_mu, d_inv, bank_prev, st.best, st.cand, T, krows(S), bank_next,
-                     bsum_next);
+  hipLaunchKernelGGL(kpp_trial_kernel, dim3(p.L.G), dim3(256), (size_t)kT * F * sizeof(float), s,
+                     d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S), p.st.best, 0, p.st.cand,
+                     (const float*)nullptr, T, krows(S), p.bank_of(c, T, S), p.bsum_of(c, T));
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
 
 int mw_kpp_indices(const void* d_ws, int64_t S, int T, int k, int64_t* d_idx_out, void* stream) {
   MW_CHECK_ARG(d_ws && d_idx_out && k >= 1 && k <= 256, "mw_kpp_indices: bad args");
-  const KppLayout L = kpp_layout(S, T);
-  char* base = reinterpret_cast<char*>(const_cast<void*>(d_ws));
-  KppState st = kpp_state(base, L, T);
+  const KppPtrs p = kpp_ptrs(d_ws, S, T);
   hipStream_t s = as_stream(stream);
   if (k >= 2) {
-    // final selection of the last step's best candidate
-    const int c = k;  // arrays of step k-1 live in bank (k-1)&1
-    double* bank = reinterpret_cast<double*>(base + L.bank) + (size_t)((c - 1) & 1) * T * S;
-    double* bsum = reinterpret_cast<double*>(base + L.bsum) + (size_t)((c - 1) & 1) * T * L.G;
-    hipLaunchKernelGGL(kpp_search_kernel, dim3(1), dim3(1024), 0, s, bank, bsum, T, S, L.G,
-                       krows(S), k - 1, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0, st.cand,
-                       st.chosen, st.best);
+    // final selection among the last step's T candidates
+    hipLaunchKernelGGL(kpp_search_kernel, dim3(1), dim3(1024), 0, s, p.bank_of(k - 1, T, S),
+                       p.bsum_of(k - 1, T), T, S, p.L.G, krows(S), k - 1, 0.0, 0.0, 0.0, 0.0, 0.0,
+                       0.0, 0.0, 0.0, 0, p.st.cand, p.st.chosen, p.st.best, -1,
+                       (const double*)nullptr);
     MW_LAUNCH_CHECK();
   }
-  MW_HIP(hipMemcpyAsync(d_idx_out, st.chosen, sizeof(int64_t) * k, hipMemcpyDeviceToDevice, s));
+  MW_HIP(hipMemcpyAsync(d_idx_out, p.st.chosen, sizeof(int64_t) * k, hipMemcpyDeviceToDevice, s));
+  return MW_OK;
+}
+
+int mw_kpp_pots(const void* d_ws, int64_t S, int T, int c, double* d_pots, void* stream) {
+  MW_CHECK_ARG(d_ws && d_pots && c >= 1 && T >= 1 && T <= 8, "mw_kpp_pots: bad args");
+  const KppPtrs p = kpp_ptrs(d_ws, S, T);
+  hipLaunchKernelGGL(kpp_pots_kernel, dim3(1), dim3(1024), 0, as_stream(stream),
+                     p.bsum_of(c - 1, T), c == 1 ? 1 : T, p.L.G, d_pots);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_kpp_search(void* d_ws, int64_t S, int T, int c, int best, const double* d_rv,
+                  int64_t* d_local_idx, void* stream) {
+  MW_CHECK_ARG(d_ws && d_rv && d_local_idx, "mw_kpp_search: null pointer");
+  MW_CHECK_ARG(c >= 1 && T >= 1 && T <= 8 && best >= 0 && best < (c == 1 ? 1 : T),
+               "mw_kpp_search: bad args (c=%d best=%d)", c, best);
+  const KppPtrs p = kpp_ptrs(d_ws, S, T);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(kpp_search_kernel, dim3(1), dim3(1024), 0, s, p.bank_of(c - 1, T, S),
+                     p.bsum_of(c - 1, T), c == 1 ? 1 : T, S, p.L.G, krows(S), 0, 0.0, 0.0, 0.0,
+                     0.0, 0.0, 0.0, 0.0, 0.0, T, p.st.cand, p.st.chosen, p.st.best, best, d_rv);
+  MW_LAUNCH_CHECK();
+  MW_HIP(hipMemcpyAsync(d_local_idx, p.st.cand, sizeof(int64_t) * T, hipMemcpyDeviceToDevice, s));
+  return MW_OK;
+}
+
+int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu, const double* d_inv, int c,
+                 int best, const float* d_rows, int T, void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_X && d_mu && d_inv && d_rows && d_ws, "mw_kpp_trial: null pointer");
+  MW_CHECK_ARG(c >= 1 && T >= 1 && T <= 8 && F <= 64 && best >= 0 && best < (c == 1 ? 1 : T),
+               "mw_kpp_trial: bad args");
+  const KppPtrs p = kpp_ptrs(d_ws, S, T);
+  hipLaunchKernelGGL(kpp_trial_kernel, dim3(p.L.G), dim3(256), (size_t)kT * F * sizeof(float),
+                     as_stream(stream), d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S),
+                     (const int*)nullptr, best, (const int64_t*)nullptr, d_rows, T, krows(S),
+                     p.bank_of(c, T, S), p.bsum_of(c, T));
+  MW_LAUNCH_CHECK();
   return MW_OK;
 }
 

@@ -7,6 +7,7 @@ import numpy as np
 import torch
 
 from . import _native as N
+from . import profiling
 
 _DTYPE_CODE = {torch.uint8: N.MW_U8, torch.int16: N.MW_U16, torch.float32: N.MW_F32}
 
@@ -105,7 +106,8 @@ def nz_stats(img: torch.Tensor):
     s = torch.empty(C, dtype=torch.float64, device=img.device)
     c = torch.empty(C, dtype=torch.int64, device=img.device)
     ws = WS.get("nz", N.query("mw_nz_stats_ws_bytes", n_pix, C))
-    N.call("mw_nz_stats", P(img), dtype_code(img), n_pix, C, P(s), P(c), P(ws), stream())
+    with profiling.timed("nz_stats", n_pix * C * img.element_size()):
+        N.call("mw_nz_stats", P(img), dtype_code(img), n_pix, C, P(s), P(c), P(ws), stream())
     return s, c
 
 
@@ -136,8 +138,9 @@ def blur(img: torch.Tensor, sigma: float, inv_mean=None, pseudoval: float = 1.0,
         out = torch.empty((H, W, C), dtype=torch.float32, device=img.device)
     wsb = N.query("mw_blur_ws_bytes", H, W, C, r)
     ws = WS.get("blur", wsb) if wsb else None
-    N.call("mw_blur", P(img), dtype_code(img), H, W, C, P(inv_mean), float(pseudoval),
-           w.ctypes.data, r, P(out), P(ws), stream())
+    with profiling.timed("blur", H * W * C * (img.element_size() + 4)):
+        N.call("mw_blur", P(img), dtype_code(img), H, W, C, P(inv_mean), float(pseudoval),
+               w.ctypes.data, r, P(out), P(ws), stream())
     return out
 
 
@@ -155,7 +158,8 @@ def mask_rank(mask_u8: torch.Tensor):
     r2p = torch.empty(n, dtype=torch.int32, device=mask_u8.device)
     cnt = torch.empty(1, dtype=torch.int64, device=mask_u8.device)
     ws = WS.get("mrank", N.query("mw_mask_rank_ws_bytes", n))
-    N.call("mw_mask_rank", P(mask_u8), n, P(r2p), P(cnt), P(ws), stream())
+    with profiling.timed("mask_rank", n):
+        N.call("mw_mask_rank", P(mask_u8), n, P(r2p), P(cnt), P(ws), stream())
     M = int(cnt.item())
     return r2p[:M], M
 
@@ -169,7 +173,9 @@ def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2
     if S == 0:
         return
     ws = WS.get("gather", N.query("mw_gather_ws_bytes", S, F))
-    N.call("mw_gather_rows", P(img_f32), C, P(feat), F, P(idx), P(r2p), S, P(X_out), P(ws), stream())
+    with profiling.timed("gather", S * (F * 4 * 2 + 8)):
+        N.call("mw_gather_rows", P(img_f32), C, P(feat), F, P(idx), P(r2p), S, P(X_out), P(ws),
+               stream())
     N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
 
 

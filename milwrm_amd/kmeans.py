@@ -22,6 +22,7 @@ import torch
 
 from . import _native as N
 from . import device as D
+from . import profiling
 from .rng import as_random_state, first_center_index, kpp_draws
 
 
@@ -127,29 +128,22 @@ def _kmeans_plusplus_device(rows: DeviceRows, k: int, random_state, n_local_tria
     first = first_center_index(S, u0)
     ws = D.WS.get("kpp", N.query("mw_kpp_ws_bytes", S, T))
     st = D.stream()
-    N.call("mw_kpp_init", D.P(rows.X), S, F, D.P(rows.mu64), D.P(rows.inv64), int(first), T,
-           D.P(ws), st)
+    with profiling.timed("kpp_init", S * (F * 4 + 8)):
+        N.call("mw_kpp_init", D.P(rows.X), S, F, D.P(rows.mu64), D.P(rows.inv64),
+               D.P(rows.X) + int(first) * F * 4, T, D.P(ws), st)
     for c in range(1, k):
         u = np.ascontiguousarray(steps[c - 1], dtype=np.float64)
-        N.call("mw_kpp_step", D.P(rows.X), S, F, D.P(rows.mu64), D.P(rows.inv64), c, u.ctypes.data,
-               T, D.P(ws), st)
+        with profiling.timed("kpp_step", S * (F * 4 + 8 + 8 * T)):
+            N.call("mw_kpp_step", D.P(rows.X), S, F, D.P(rows.mu64), D.P(rows.inv64), c,
+                   u.ctypes.data, T, D.P(ws), st)
     idx = torch.empty(k, dtype=torch.int64, device=rows.X.device)
     N.call("mw_kpp_indices", D.P(ws), S, T, k, D.P(idx), st)
     idx = idx.cpu().numpy()
+    idx[0] = first
     return rows.scaled_rows(idx), idx
 
 
-class _Collective:
-    """Cross-rank reduction hook (identity on one device)."""
-
-    def all_reduce_(self, t: torch.Tensor):
-        return t
-
-    def farthest(self, rows, labels, centers_old, n):  # pragma: no cover - see dist.py
-        raise NotImplementedError
-
-
-LOCAL = _Collective()
+from .dist import LOCAL_COMM as LOCAL  # noqa: E402
 
 
 def _relocate_empty(rows: DeviceRows, labels: torch.Tensor, centers_old, centers_new, weight,
@@ -159,7 +153,7 @@ def _relocate_empty(rows: DeviceRows, labels: torch.Tensor, centers_old, centers
     n_empty = empty.size
     if n_empty == 0:
         return
-    if comm is not LOCAL:
+    if comm.sharded():
         far_idx, far_val, xs, old_lab = comm.farthest(rows, labels, centers_old, n_empty)
     else:
         S, F = rows.S, rows.F
@@ -212,8 +206,9 @@ def lloyd_device(rows: DeviceRows, centers_init: np.ndarray, max_iter=300, tol=0
     def step(mode):
         pin.numpy()[:] = centers
         c32.copy_(pin, non_blocking=True)
-        N.call("mw_lloyd_step", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(c32), k,
-               D.P(labels), mode, D.P(ws), st)
+        with profiling.timed(f"lloyd_step_mode{mode}", S * (F * 4 + (2 if mode < 2 else 1))):
+            N.call("mw_lloyd_step", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(c32), k,
+                   D.P(labels), mode, D.P(ws), st)
         N.call("mw_lloyd_reduce", D.P(ws), S, k, F, D.P(out), st)
         comm.all_reduce_(out)
         return out.cpu().numpy()
@@ -285,7 +280,8 @@ class KMeans:
         if self.n_clusters > 64:
             raise NotImplementedError("n_clusters > 64 is not supported by the device kernels")
 
-    def fit(self, X, y=None, sample_weight=None, comm=LOCAL):
+    def fit(self, X, y=None, sample_weight=None, comm=None):
+        comm = LOCAL if comm is None else comm
         if sample_weight is not None and not np.all(np.asarray(sample_weight) == 1):
             raise NotImplementedError("non-unit sample_weight")
         rows = X if isinstance(X, DeviceRows) else DeviceRows.from_host(X)
@@ -312,8 +308,13 @@ class KMeans:
                                      f"match the number of clusters {k} / features {rows.F}.")
                 self.init_indices_ = None
             elif init == "k-means++":
-                centers0, self.init_indices_ = _kmeans_plusplus_device(rows, k, rs)
+                if comm.sharded():
+                    centers0, self.init_indices_ = comm.kpp(rows, k, rs)
+                else:
+                    centers0, self.init_indices_ = _kmeans_plusplus_device(rows, k, rs)
             elif init == "random":
+                if comm.sharded():
+                    raise NotImplementedError("init='random' with sharded rows")
                 seeds = rs.choice(rows.S, size=k, replace=False,
                                   p=np.full(rows.S, 1.0 / rows.S))
                 centers0, self.init_indices_ = rows.scaled_rows(seeds), seeds

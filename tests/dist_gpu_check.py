@@ -1,0 +1,69 @@
+"""Sharded-fit equivalence on the GPU box (launched with torchrun, 2 ranks on
+one GPU, gloo for the small messages):  each rank preprocesses its own slide,
+the fit runs sharded (k-means++ across shards, all-reduced Lloyd partials);
+rank 0 then repeats the whole pipeline single-process over both slides and
+compares init indices, iterations, centers, inertia and per-slide labels.
+
+  torchrun --nproc-per-node 2 --master-addr 127.0.0.1 tests/dist_gpu_check.py
+"""
+import os
+import sys
+
+import numpy as np
+import pandas as pd
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def labeler_for(slides, comm=None):
+    import milwrm_amd as M
+
+    imgs = [M.img(r.copy(), mask=m.copy()) for r, m in slides]
+    ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
+    df = pd.DataFrame({"Img": imgs, "batch_names": ["b"] * len(imgs), "mean estimators": list(ests),
+                       "pixels": list(pix)})
+    lab = M.mxif_labeler(df)
+    lab.prep_cluster_data(features=list(range(8)), sigma=2, fract=0.2, comm=comm)
+    lab.label_tissue_regions(k=6, plot_out=False, random_state=18, comm=comm)
+    return lab
+
+
+def main():
+    from milwrm_amd.dist import DistComm
+    from oracle.milwrm_oracle import synth_slide
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    slides = [synth_slide(160, 192, 8, seed=100 + r, mode="hard") for r in range(world)]
+    comm = DistComm(device=torch.device("cpu"))
+    lab = labeler_for([slides[rank]], comm)
+    res = dict(idx=lab.kmeans.init_indices_, n_iter=lab.kmeans.n_iter_,
+               centers=lab.kmeans.cluster_centers_, inertia=lab.kmeans.inertia_,
+               tid=np.nan_to_num(lab.tissue_IDs[0], nan=-1))
+    allres = [None] * world
+    dist.all_gather_object(allres, res)
+    ok = True
+    if rank == 0:
+        ref = labeler_for(slides, None)
+        checks = {
+            "init_indices": np.array_equal(ref.kmeans.init_indices_, allres[0]["idx"]),
+            "n_iter": ref.kmeans.n_iter_ == allres[0]["n_iter"],
+            "centers": np.max(np.abs(ref.kmeans.cluster_centers_ - allres[0]["centers"])) < 1e-6,
+            "inertia": abs(ref.kmeans.inertia_ - allres[0]["inertia"]) / ref.kmeans.inertia_ < 1e-9,
+            "same_on_ranks": all(np.array_equal(a["centers"], allres[0]["centers"]) for a in allres),
+            "labels": all(np.array_equal(np.nan_to_num(ref.tissue_IDs[r], nan=-1), allres[r]["tid"])
+                          for r in range(world)),
+        }
+        ok = all(checks.values())
+        print("dist_gpu_check", "PASS" if ok else "FAIL", checks, flush=True)
+    flag = [ok]
+    dist.broadcast_object_list(flag, src=0)
+    dist.destroy_process_group()
+    sys.exit(0 if flag[0] else 1)
+
+
+if __name__ == "__main__":
+    main()
