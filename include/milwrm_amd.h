@@ -73,8 +73,9 @@ int mw_lognorm(const void* d_img, int dtype, int64_t n_pix, int C,
  * Separable Gaussian, per channel, edge-replicate ('nearest'), radius r =
  * int(4*sigma+0.5) <= 32, taps h_w[0..2r] (scipy _gaussian_kernel1d).
  * Optional fused log-normalise prologue when d_inv_mean != NULL.  HWC in,
- * HWC fp32 out (out must not alias in).  r <= 12: single streaming pass
- * (register ring); r > 12: two passes through d_ws (mw_blur_ws_bytes). */
+ * HWC fp32 out (out must not alias in).  Even C and r <= 12: single
+ * streaming pass (register ring); otherwise two passes through d_ws
+ * (mw_blur_ws_bytes). */
 size_t mw_blur_ws_bytes(int H, int W, int C, int radius);
 int mw_blur(const void* d_img, int dtype, int H, int W, int C,
             const float* d_inv_mean, float pseudoval,
@@ -111,6 +112,21 @@ int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats,
  * Bit-exact np.random.RandomState(seed).randint(0, high, size) (== choice),
  * masked rejection on MT19937.  Host implementation (single thread). */
 int mw_legacy_randint_host(uint32_t seed, int64_t high, int64_t size, int32_t* h_out);
+
+/* ---- device MT19937 with jump-ahead (bit-exact legacy randint) -------------
+ * One-time host tables: h_j(t) = t^(L*2^j) mod phi(t), j < J (312 uint64 per
+ * polynomial; phi = characteristic polynomial of the MT19937 transition,
+ * found by Berlekamp-Massey).  The device builds the start state of every
+ * L-word segment by a parallel prefix of jumps (block Horner), then every
+ * workgroup regenerates, tempers and filters its segment; accepted draws are
+ * compacted in stream order.  Output identical to mw_legacy_randint_host. */
+int mw_mt_jump_tables(int64_t L, int J, uint64_t* h_tables);
+int mw_mt_jump_host(const uint32_t* h_state_in, const uint64_t* h_poly, uint32_t* h_state_out);
+int mw_mt_seed_state(uint32_t seed, uint32_t* h_state);
+size_t mw_legacy_randint_ws_bytes(int64_t high, int64_t size, int64_t L);
+int mw_legacy_randint_device(uint32_t seed, int64_t high, int64_t size, const uint64_t* d_tables,
+                             int J, int64_t L, int32_t* d_out, int64_t* d_total, void* d_ws,
+                             void* stream);
 
 /* ---- k-means++ (sklearn _kmeans.py:174-272) ---------------------------------
  * Rows are scaled on the fly: x' = (x - mu) * inv_sigma  (fp64 affine).

@@ -27,6 +27,7 @@ from .kmeans import DeviceRows, KMeans, StandardScaler
 from .MxIF import checktype, img
 from .ST import blur_features_st
 from .dist import LOCAL_COMM
+from .rng import check_total, subsample_indices_device
 
 
 # ------------------------------------------------------------ k selection
@@ -307,19 +308,18 @@ class mxif_labeler(tissue_labeler):
         # phase 2: fused lognorm+blur, gather rows into X (image_df order)
         off = 0
         paths = []
+        totals = []
         for n_img, (im, batch, (r2p, M), S) in enumerate(
                 zip(images, self.image_df["batch_names"], ranks, counts)):
             im.log_normalize(mean=means[batch])
             im.blurring(filter_name=filter_name, sigma=sigma)
             np.random.seed(16)
             if S:
-                from .rng import subsample_indices
-
-                idx = subsample_indices(M, fract, 16)
-                feat = torch.as_tensor(np.asarray(im._features(features), dtype=np.int32), device=dev)
-                D.gather_rows(D.as_float32(im._device()), feat,
-                              torch.from_numpy(idx).to(dev, non_blocking=True), r2p,
-                              X[off:off + S], stats, accumulate=off > 0)
+                idx, tot = subsample_indices_device(M, fract, 16, dev)
+                totals.append((tot, S))
+                feat = D.h2d(np.asarray(im._features(features), dtype=np.int32), dev)
+                D.gather_rows(D.as_float32(im._device()), feat, idx, r2p, X[off:off + S], stats,
+                              accumulate=off > 0)
             off += S
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))
@@ -328,6 +328,8 @@ class mxif_labeler(tissue_labeler):
             self.image_df["Img"] = paths
         else:
             self._images = images
+        for tot, S in totals:
+            check_total(tot, S)
         st = comm.merge_stats(stats.cpu().numpy(), F)
         self.scaler = StandardScaler.from_stats(st)
         mu, inv = self.scaler.affine()

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from . import device as D
-from .rng import subsample_indices
+from .rng import check_total, subsample_indices_device
 
 
 def checktype(obj):
@@ -305,7 +305,7 @@ class img:
         mean = np.asarray(mean, dtype=np.float64)
         with np.errstate(divide="ignore"):
             inv = (1.0 / mean).astype(np.float32)
-        self._pending = (torch.from_numpy(inv).to(D.device()), float(pseudoval))
+        self._pending = (D.h2d(inv, D.device()), float(pseudoval))
         self._host64 = None
 
     def _subsample_device(self, features, fract=0.2, random_state=16, X_out=None, stats=None,
@@ -316,17 +316,17 @@ class img:
         np.random.seed(random_state)  # the reference's global-RNG side effect (MxIF.py:484)
         src = D.as_float32(self._materialize())
         r2p, M = D.mask_rank(self._mask_device().reshape(-1))
-        idx = subsample_indices(M, fract, random_state)
-        S = idx.shape[0]
         dev = src.device
+        d_idx, total = subsample_indices_device(M, fract, random_state, dev)
+        S = d_idx.shape[0]
         if X_out is None:
             X_out = torch.empty((S, len(features)), dtype=torch.float32, device=dev)
         if stats is None:
             stats = torch.zeros(1 + 2 * len(features), dtype=torch.float64, device=dev)
         if S:
-            d_idx = torch.from_numpy(idx).to(dev, non_blocking=True)
-            feat = torch.as_tensor(np.asarray(features, dtype=np.int32), device=dev)
+            feat = D.h2d(np.asarray(features, dtype=np.int32), dev)
             D.gather_rows(src, feat, d_idx, r2p, X_out, stats, accumulate)
+            check_total(total, S)
         return X_out, stats
 
     def subsample_pixels(self, features, fract=0.2, random_state=16):

@@ -43,6 +43,11 @@ _PROTOS = {
     "mw_gather_rows": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "mw_col_stats_finalize": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),
     "mw_legacy_randint_host": (c_i32, [c_u32, c_i64, c_i64, c_vp]),
+    "mw_mt_jump_tables": (c_i32, [c_i64, c_i32, c_vp]),
+    "mw_mt_jump_host": (c_i32, [c_vp, c_vp, c_vp]),
+    "mw_mt_seed_state": (c_i32, [c_u32, c_vp]),
+    "mw_legacy_randint_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "mw_legacy_randint_device": (c_i32, [c_u32, c_i64, c_i64, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mw_kpp_ws_bytes": (c_sz, [c_i64, c_i32]),
     "mw_kpp_init": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "mw_kpp_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),

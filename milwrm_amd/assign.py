@@ -20,11 +20,11 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
     H, W, C = img_f32.shape
     k, F = centers.shape
     dev = img_f32.device
-    feat = torch.as_tensor(np.asarray(feat_idx, dtype=np.int32), device=dev)
-    a = torch.from_numpy(np.asarray(inv, dtype=np.float64).astype(np.float32)).to(dev)
-    b = torch.from_numpy((-np.asarray(mu, dtype=np.float64) * np.asarray(inv, dtype=np.float64))
-                         .astype(np.float32)).to(dev)
-    c32 = torch.from_numpy(np.ascontiguousarray(centers, dtype=np.float32)).to(dev)
+    feat = D.h2d(np.asarray(feat_idx, dtype=np.int32), dev)
+    a = D.h2d(np.asarray(inv, dtype=np.float64).astype(np.float32), dev)
+    b = D.h2d((-np.asarray(mu, dtype=np.float64) * np.asarray(inv, dtype=np.float64))
+              .astype(np.float32), dev)
+    c32 = D.h2d(np.asarray(centers, dtype=np.float32), dev)
     n = H * W
     lab = torch.empty((H, W), dtype=torch.int8, device=dev)
     conf = torch.empty((H, W), dtype=torch.float32, device=dev)

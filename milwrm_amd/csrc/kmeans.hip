@@ -32,13 +32,27 @@ static inline int64_t krows(int64_t n) {
   return ((tiles + g - 1) / g) * kT;
 }
 
-// coalesced copy of `n` consecutive floats into LDS (16-B vectors + tail)
+// coalesced copy of `n` consecutive floats into LDS: 16-B vectors issued in
+// batches of 8 per thread (all loads in flight before the first LDS store),
+// then the tail.
 __device__ __forceinline__ void stage(const float* __restrict__ src, int n, float* dst) {
   const int n4 = n >> 2;
   const float4* s4 = reinterpret_cast<const float4*>(src);
   float4* d4 = reinterpret_cast<float4*>(dst);
-  for (int q = threadIdx.x; q < n4; q += blockDim.x) d4[q] = s4[q];
-  for (int q = (n4 << 2) + threadIdx.x; q < n; q += blockDim.x) dst[q] = src[q];
+  const int nt = blockDim.x;
+  for (int q0 = threadIdx.x; q0 < n4; q0 += 8 * nt) {
+    float4 r[8];
+    // unconditional loads from clamped (valid) addresses: a guarded load makes
+    // hipcc branch around it and wait vmcnt(0) per element
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = s4[min(q0 + i * nt, n4 - 1)];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = q0 + i * nt;
+      if (q < n4) d4[q] = r[i];
+    }
+  }
+  for (int q = (n4 << 2) + threadIdx.x; q < n; q += nt) dst[q] = src[q];
 }
 
 // ===================================================================== kpp
@@ -205,25 +219,34 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(const double* __restri
     const int64_t c_lo = lo + t * per, c_hi = min(hi, c_lo + per);
     double part = 0.0;
     for (int64_t i = c_lo; i < c_hi; ++i) part += d[i];
+    // inclusive scan of the chunk sums (fixed order), base-offset
     s_chunk[t] = part;
     __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const double v = t >= o ? s_chunk[t - o] : 0.0;
+      __syncthreads();
+      s_chunk[t] += v;
+      __syncthreads();
+    }
+    if (t == 0) s_found = -1;
+    __syncthreads();
+    {
+      const double incl = base + s_chunk[t];
+      const double excl = base + (t > 0 ? s_chunk[t - 1] : 0.0);
+      if (c_lo < c_hi && incl >= rv && (t == 0 || excl < rv)) s_found = t;
+    }
+    __syncthreads();
     if (t == 0) {
-      double run = base;
       int64_t idx = hi - 1;  // rounding fallback: clip to the block's end
-      for (int q = 0; q < 1024; ++q) {
-        const int64_t ql = lo + q * per;
-        if (ql >= hi) break;
-        if (run + s_chunk[q] >= rv) {
-          const int64_t qh = min(hi, ql + per);
-          double r2 = run;
-          idx = qh - 1;
-          for (int64_t i = ql; i < qh; ++i) {
-            r2 += d[i];
-            if (r2 >= rv) { idx = i; break; }
-          }
-          break;
+      const int q = s_found;
+      if (q >= 0) {
+        const int64_t ql = lo + q * per, qh = min(hi, ql + per);
+        double r2 = base + (q > 0 ? s_chunk[q - 1] : 0.0);
+        idx = qh - 1;
+        for (int64_t i = ql; i < qh; ++i) {
+          r2 += d[i];
+          if (r2 >= rv) { idx = i; break; }
         }
-        run += s_chunk[q];
       }
       if (idx > S - 1) idx = S - 1;
       if (idx < 0) idx = 0;
@@ -476,12 +499,30 @@ __global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X,
   }
 }
 
-__global__ void lloyd_reduce_kernel(const double* __restrict__ rec, int G, int rl,
-                                    double* __restrict__ out) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < rl; q += gridDim.x * blockDim.x) {
-    double s = 0.0;
-    for (int b = 0; b < G; ++b) s += rec[(size_t)b * rl + q];
-    out[q] = s;
+// fixed-order sum of G per-block records: thread (q, part) sums blocks
+// b = part, part+8, ... with 8 independent partial sums, then parts combine
+// in order.
+__global__ void __launch_bounds__(256) lloyd_reduce_kernel(const double* __restrict__ rec, int G,
+                                                           int rl, double* __restrict__ out) {
+  __shared__ double s[8][33];
+  const int lane = threadIdx.x & 31, part = threadIdx.x >> 5;  // 32 columns x 8 parts
+  const int q = blockIdx.x * 32 + lane;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (q < rl) {
+    int b = part;
+    for (; b + 24 < G; b += 32) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += rec[(size_t)(b + 8 * u) * rl + q];
+    }
+    for (; b < G; b += 8) acc[0] += rec[(size_t)b * rl + q];
+  }
+  s[part][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (part == 0 && q < rl) {
+    double t = 0.0;
+#pragma unroll
+    for (int p2 = 0; p2 < 8; ++p2) t += s[p2][lane];
+    out[q] = t;
   }
 }
 
@@ -796,7 +837,7 @@ int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a, const fl
 int mw_lloyd_reduce(const void* d_ws, int64_t S, int k, int F, double* d_out, void* stream) {
   MW_CHECK_ARG(d_ws && d_out, "mw_lloyd_reduce: null pointer");
   const int rl = lloyd_rec(k, F);
-  hipLaunchKernelGGL(lloyd_reduce_kernel, dim3((rl + 255) / 256), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(lloyd_reduce_kernel, dim3((rl + 31) / 32), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), kblocks(S), rl, d_out);
   MW_LAUNCH_CHECK();
   return MW_OK;
@@ -871,7 +912,7 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
 
 int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom, void* stream) {
   MW_CHECK_ARG(d_ws && d_dom && k >= 1, "mw_assign_reduce: bad args");
-  hipLaunchKernelGGL(lloyd_reduce_kernel, dim3((2 * k + 255) / 256), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(lloyd_reduce_kernel, dim3((2 * k + 31) / 32), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), kblocks(n_pix), 2 * k, d_dom);
   MW_LAUNCH_CHECK();
   return MW_OK;

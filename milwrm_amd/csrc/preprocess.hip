@@ -83,6 +83,20 @@ __global__ void __launch_bounds__(256) nz_stats_kernel(const T* __restrict__ img
   if (t < teff) {
     const int64_t stride = (int64_t)teff * V;
     int64_t e = lo + (int64_t)t * V;
+    // four independent 16-B loads in flight per iteration
+    for (; e + 3 * stride + V <= hi; e += 4 * stride) {
+      Pack<T, V> p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p[u] = *reinterpret_cast<const Pack<T, V>*>(img + e + u * stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          const bool nz = p[u].v[i] != T(0);
+          acc[i] += nz ? (double)(float)p[u].v[i] : 0.0;
+          cnt[i] += nz ? 1 : 0;
+        }
+    }
     for (; e + V <= hi; e += stride) {
       Pack<T, V> p = *reinterpret_cast<const Pack<T, V>*>(img + e);
 #pragma unroll
@@ -122,13 +136,21 @@ __global__ void nz_stats_reduce(const double* __restrict__ part, int G, int C,
                                 double* __restrict__ sum, int64_t* __restrict__ cnt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, n = 0.0;
-  for (int b = 0; b < G; ++b) {
-    s += part[(size_t)b * 2 * C + c];
-    n += part[(size_t)b * 2 * C + C + c];
+  double s[4] = {0, 0, 0, 0}, n[4] = {0, 0, 0, 0};
+  int b = 0;
+  for (; b + 3 < G; b += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s[u] += part[(size_t)(b + u) * 2 * C + c];
+      n[u] += part[(size_t)(b + u) * 2 * C + C + c];
+    }
   }
-  sum[c] = s;
-  cnt[c] = (int64_t)n;
+  for (; b < G; ++b) {
+    s[0] += part[(size_t)b * 2 * C + c];
+    n[0] += part[(size_t)b * 2 * C + C + c];
+  }
+  sum[c] = (s[0] + s[1]) + (s[2] + s[3]);
+  cnt[c] = (int64_t)((n[0] + n[1]) + (n[2] + n[3]));
 }
 
 static inline int gcd_i(int a, int b) { while (b) { int t = a % b; a = b; b = t; } return a; }
@@ -174,14 +196,23 @@ __global__ void lognorm_kernel(const T* __restrict__ img, int64_t n_elem, int C,
 constexpr int kMaxRadius = 32;
 struct BlurTaps { float w[2 * kMaxRadius + 1]; };
 
-constexpr int kEPT = 4;     // output elements per thread per row
-constexpr int kMaxL = 12;   // input-row loads per thread per row (static bound)
-constexpr int kBlurBH = 128;
+constexpr int kPPT = 2;     // output element PAIRS per thread per row
+constexpr int kMaxL = 8;    // input-row pair loads per thread per row (static bound)
+constexpr int kBlurBH = 256;
 
+template <typename T> struct Pair2;
+template <> struct Pair2<uint8_t> { using type = uchar2; };
+template <> struct Pair2<uint16_t> { using type = ushort2; };
+template <> struct Pair2<float> { using type = float2; };
+
+// Requires C even: element pairs (2p, 2p+1) never straddle a pixel, so every
+// LDS / global access below is an aligned 8-byte (fp32) or 2-element load and
+// consecutive lanes touch consecutive pairs (conflict-free ds_read_b64).
 template <typename T, int R>
 __global__ void __launch_bounds__(1024) blur_kernel(const T* __restrict__ in, int H, int W, int C, int BW,
                                                     const float* __restrict__ inv_mean, float pseudo,
                                                     BlurTaps taps, float* __restrict__ out) {
+  using P2 = typename Pair2<T>::type;
   constexpr int NR = 2 * R + 1;
   extern __shared__ __attribute__((aligned(16))) float s_row[];  // 2 x (BW+2R)*C
   const int t = threadIdx.x;
@@ -190,57 +221,69 @@ __global__ void __launch_bounds__(1024) blur_kernel(const T* __restrict__ in, in
   const int y0 = blockIdx.y * kBlurBH;
   const int y1 = min(H, y0 + kBlurBH);
   const int bw = min(BW, W - x0);
-  const int seg = (bw + 2 * R) * C;  // halo'd row elements
+  const int seg2 = (bw + 2 * R) * C / 2;  // halo'd row pairs
   const int rowcap = (BW + 2 * R) * C;
   const int nrows = (y1 - y0) + 2 * R;
   const bool logn = inv_mean != nullptr;
+  const int npairs = bw * C / 2;
 
-  // this thread's output elements (fixed for every row)
-  int e_pos[kEPT];
-  bool e_ok[kEPT];
+  // output pairs p = t + i*nt (strided: lanes read/write consecutive pairs)
+  int e_pos[kPPT];
+  bool e_ok[kPPT];
 #pragma unroll
-  for (int i = 0; i < kEPT; ++i) {
-    const int e = t * kEPT + i;
-    e_ok[i] = e < bw * C;
-    e_pos[i] = e_ok[i] ? e : 0;
+  for (int i = 0; i < kPPT; ++i) {
+    const int p = t + i * nt;
+    e_ok[i] = p < npairs;
+    e_pos[i] = e_ok[i] ? 2 * p : 0;
   }
-  // this thread's input-row load slots (fixed for every row): source element
-  // offset inside the row (edge-clamped column) and the channel's 1/mean
+  // input load slots (pairs), fixed for every row
   int l_src[kMaxL];
-  float l_inv[kMaxL];
+  float2 l_inv[kMaxL];
 #pragma unroll
   for (int k = 0; k < kMaxL; ++k) {
-    const int q = t + k * nt;
+    const int q = t + k * nt;  // pair index in the halo'd row
     l_src[k] = -1;
-    l_inv[k] = 1.f;
-    if (q < seg) {
-      const int px = q / C;
-      const int c = q - px * C;
+    l_inv[k] = make_float2(1.f, 1.f);
+    if (q < seg2) {
+      const int e = 2 * q;
+      const int px = e / C;
+      const int c = e - px * C;
       int gx = x0 - R + px;
       gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
       l_src[k] = gx * C + c;
-      if (inv_mean) l_inv[k] = inv_mean[c];
+      if (logn) l_inv[k] = make_float2(inv_mean[c], inv_mean[c + 1]);
     }
   }
-  float ring[kEPT][NR];
+  float2 ring[kPPT][NR];
 #pragma unroll
-  for (int i = 0; i < kEPT; ++i)
+  for (int i = 0; i < kPPT; ++i)
 #pragma unroll
-    for (int j = 0; j < NR; ++j) ring[i][j] = 0.f;
+    for (int j = 0; j < NR; ++j) ring[i][j] = make_float2(0.f, 0.f);
 
-  float pre[kMaxL];
+  float2 pre[kMaxL];
   auto fetch_row = [&](int rr) {
     int yy = y0 - R + rr;
     yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
     const T* src = in + (int64_t)yy * W * C;
 #pragma unroll
-    for (int k = 0; k < kMaxL; ++k) pre[k] = l_src[k] >= 0 ? (float)src[l_src[k]] : 0.f;
+    for (int k = 0; k < kMaxL; ++k) {
+      const P2 v = *reinterpret_cast<const P2*>(src + (l_src[k] >= 0 ? l_src[k] : 0));
+      pre[k] = make_float2((float)v.x, (float)v.y);
+    }
   };
   auto store_row = [&](int buf) {
-    float* dst = s_row + buf * rowcap;
+    float2* dst = reinterpret_cast<float2*>(s_row + buf * rowcap);
 #pragma unroll
-    for (int k = 0; k < kMaxL; ++k)
-      if (l_src[k] >= 0) dst[t + k * nt] = logn ? lognorm1(pre[k], l_inv[k], pseudo) : pre[k];
+    for (int k = 0; k < kMaxL; ++k) {
+      if (l_src[k] >= 0) {
+        float2 v = pre[k];
+        if (logn) {
+          v.x = lognorm1(v.x, l_inv[k].x, pseudo);
+          v.y = lognorm1(v.y, l_inv[k].y, pseudo);
+        }
+        dst[t + k * nt] = v;
+      }
+    }
   };
 
   fetch_row(0);
@@ -255,21 +298,29 @@ __global__ void __launch_bounds__(1024) blur_kernel(const T* __restrict__ in, in
         if (more) fetch_row(rr + 1);  // global loads in flight during the compute
         const float* row = s_row + (rr & 1) * rowcap;
 #pragma unroll
-        for (int i = 0; i < kEPT; ++i) {
-          float h = 0.f;
+        for (int i = 0; i < kPPT; ++i) {
+          float2 h = make_float2(0.f, 0.f);
 #pragma unroll
-          for (int j = 0; j < NR; ++j) h = fmaf(taps.w[j], row[e_pos[i] + j * C], h);
+          for (int j = 0; j < NR; ++j) {
+            const float2 v = *reinterpret_cast<const float2*>(row + e_pos[i] + j * C);
+            h.x = fmaf(taps.w[j], v.x, h.x);
+            h.y = fmaf(taps.w[j], v.y, h.y);
+          }
           ring[i][s] = h;
         }
         if (rr >= 2 * R) {
           const int y = y0 + rr - 2 * R;
           float* orow = out + ((int64_t)y * W + x0) * C;
 #pragma unroll
-          for (int i = 0; i < kEPT; ++i) {
-            float v = 0.f;
+          for (int i = 0; i < kPPT; ++i) {
+            float2 v = make_float2(0.f, 0.f);
 #pragma unroll
-            for (int j = 0; j < NR; ++j) v = fmaf(taps.w[j], ring[i][(s + 1 + j) % NR], v);
-            if (e_ok[i]) orow[e_pos[i]] = v;
+            for (int j = 0; j < NR; ++j) {
+              const float2 r2 = ring[i][(s + 1 + j) % NR];
+              v.x = fmaf(taps.w[j], r2.x, v.x);
+              v.y = fmaf(taps.w[j], r2.y, v.y);
+            }
+            if (e_ok[i]) *reinterpret_cast<float2*>(orow + e_pos[i]) = v;
           }
         }
         if (more) store_row((rr + 1) & 1);
@@ -283,13 +334,13 @@ template <typename T, int R>
 static int launch_blur_r(const T* in, int H, int W, int C, const float* inv_mean, float p,
                          const BlurTaps& taps, float* out, hipStream_t st) {
   int BW = 64;
-  while (BW > 1 && (BW * C + kEPT - 1) / kEPT > 1024) BW >>= 1;
-  MW_CHECK_ARG((BW * C + kEPT - 1) / kEPT <= 1024, "mw_blur: C=%d too large", C);
-  int nt = (BW * C + kEPT - 1) / kEPT;
+  while (BW > 1 && (BW * C / 2 + kPPT - 1) / kPPT > 1024) BW >>= 1;
+  int nt = (BW * C / 2 + kPPT - 1) / kPPT;
   nt = ((nt + 63) / 64) * 64;
+  MW_CHECK_ARG(nt <= 1024, "mw_blur: C=%d too large", C);
   const size_t lds = 2 * (size_t)(BW + 2 * R) * C * sizeof(float);
   MW_CHECK_ARG(lds <= 160 * 1024, "mw_blur: LDS %zu too large (C=%d, r=%d)", lds, C, R);
-  MW_CHECK_ARG((BW + 2 * R) * C <= kMaxL * nt, "mw_blur: row segment exceeds load slots (C=%d r=%d)", C, R);
+  MW_CHECK_ARG((BW + 2 * R) * C / 2 <= kMaxL * nt, "mw_blur: row segment exceeds load slots (C=%d r=%d)", C, R);
   dim3 grid((W + BW - 1) / BW, (H + kBlurBH - 1) / kBlurBH);
   hipLaunchKernelGGL((blur_kernel<T, R>), grid, dim3(nt), lds, st, in, H, W, C, BW, inv_mean, p,
                      taps, out);
@@ -346,7 +397,7 @@ constexpr int kRingMax = 12;
 template <typename T>
 static int launch_blur(const T* in, int H, int W, int C, const float* inv_mean, float p,
                        const BlurTaps& taps, int r, float* out, float* tmp, hipStream_t st) {
-  switch (r) {
+  switch ((C % 2 == 0) ? r : -1) {
 #define MW_R(N) case N: return launch_blur_r<T, N>(in, H, W, C, inv_mean, p, taps, out, st);
     MW_R(0) MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8) MW_R(9) MW_R(10)
     MW_R(11) MW_R(12)
@@ -502,23 +553,40 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
                                                      int64_t R, float* __restrict__ X,
                                                      double* __restrict__ rec) {
   extern __shared__ __attribute__((aligned(16))) float s_tile[];  // 256*F floats + stats scratch
-  __shared__ int s_feat[256];
-  const int t = threadIdx.x;
-  for (int f = t; f < F; f += 256) s_feat[f] = feat[f];
+  __shared__ int s_feat[64];
+  __shared__ uint32_t s_pix[256];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  for (int f = t; f < 64; f += 256) s_feat[f] = f < F ? feat[f] : 0;
   const int nparts = 256 / F;
   const bool st_on = t < nparts * F;
   const int sf = st_on ? t % F : 0, spart = st_on ? t / F : 0;
   double n_acc = 0.0, m_acc = 0.0, q_acc = 0.0;
+  // cooperative row loads: a wave instruction covers RPI rows x FP features
+  const int FP = F <= 32 ? 32 : 64;
+  const int RPI = 64 / FP;
+  const int lf = lane % FP, lr = lane / FP;
   const int64_t lo = (int64_t)blockIdx.x * R;
   const int64_t hi = min(S, lo + R);
   __syncthreads();
+  const int fcol = lf < F ? s_feat[lf] : 0;
   for (int64_t r0 = lo; r0 < hi; r0 += kTile) {
     const int nrow = (int)min((int64_t)kTile, hi - r0);
-    if (t < nrow) {
-      const int64_t j = r0 + t;
-      const uint32_t p = r2p[idx[j]];
-      const float* src = img + (int64_t)p * C;
-      for (int f = 0; f < F; ++f) s_tile[t * F + f] = src[s_feat[f]];
+    if (t < nrow) s_pix[t] = r2p[idx[r0 + t]];
+    __syncthreads();
+    // wave wid loads rows [wid*64, wid*64+64) of the tile, RPI rows per instruction
+    constexpr int kBatch = 16;
+    for (int i0 = 0; i0 < 64 / RPI; i0 += kBatch) {
+      float v[kBatch];
+#pragma unroll
+      for (int i = 0; i < kBatch; ++i) {
+        const int row = min(wid * 64 + (i0 + i) * RPI + lr, nrow - 1);  // clamped: always valid
+        v[i] = img[(int64_t)s_pix[row] * C + fcol];
+      }
+#pragma unroll
+      for (int i = 0; i < kBatch; ++i) {
+        const int row = wid * 64 + (i0 + i) * RPI + lr;
+        if (i0 + i < 64 / RPI && row < nrow && lf < F) s_tile[row * F + lf] = v[i];
+      }
     }
     __syncthreads();
     // coalesced write of the tile (rows contiguous in X)
@@ -562,22 +630,50 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   }
 }
 
-__global__ void col_stats_kernel(const double* __restrict__ rec, int G, int F, double* __restrict__ st,
-                                 int accumulate) {
-  const int f = threadIdx.x;
-  double n = 0.0, m = 0.0, q = 0.0;
+// Merge per-block (n, mean, M2) records: n = sum n_b, mean = sum n_b m_b / n,
+// M2 = sum [M2_b + n_b (m_b - mean)^2]  (fixed order; optional prior record).
+__global__ void __launch_bounds__(256) col_stats_kernel(const double* __restrict__ rec, int G, int F,
+                                                        double* __restrict__ st, int accumulate) {
+  __shared__ double s_n[4][64], s_s[4][64], s_mean[64];
+  const int f = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int rl = 1 + 2 * F;
+  double n = 0.0, sm = 0.0, q = 0.0;
+  double n0 = 0.0, m0 = 0.0, q0 = 0.0;
+  if (accumulate && f < F) { n0 = st[0]; m0 = st[1 + f]; q0 = st[1 + F + f]; }
+  if (f < F)
+    for (int b = part; b < G; b += 4) {
+      const double nb = rec[(size_t)b * rl];
+      n += nb;
+      sm += nb * rec[(size_t)b * rl + 1 + f];
+    }
+  s_n[part][f] = n;
+  s_s[part][f] = sm;
+  __syncthreads();
+  if (part == 0 && f < F) {
+    double N = n0, SM = n0 * m0;
+    for (int p2 = 0; p2 < 4; ++p2) { N += s_n[p2][f]; SM += s_s[p2][f]; }
+    s_mean[f] = N > 0 ? SM / N : 0.0;
+    s_n[0][f] = N;
+  }
+  __syncthreads();
   if (f < F) {
-    if (accumulate) { n = st[0]; m = st[1 + f]; q = st[1 + F + f]; }
-    for (int b = 0; b < G; ++b) {
-      const double* r = rec + (size_t)b * (1 + 2 * F);
-      chan_merge(n, m, q, r[0], r[1 + f], r[1 + F + f]);
+    const double mean = s_mean[f];
+    for (int b = part; b < G; b += 4) {
+      const double nb = rec[(size_t)b * rl];
+      const double d = rec[(size_t)b * rl + 1 + f] - mean;
+      q += rec[(size_t)b * rl + 1 + F + f] + nb * d * d;
     }
   }
-  __syncthreads();  // every thread has read st[0] before it is rewritten
-  if (f < F) {
-    if (f == 0) st[0] = n;
-    st[1 + f] = m;
-    st[1 + F + f] = q;
+  __syncthreads();
+  s_s[part][f] = q;
+  __syncthreads();
+  if (part == 0 && f < F) {
+    const double mean = s_mean[f];
+    double Q = n0 > 0 ? q0 + n0 * (m0 - mean) * (m0 - mean) : 0.0;
+    for (int p2 = 0; p2 < 4; ++p2) Q += s_s[p2][f];
+    if (f == 0) st[0] = s_n[0][0];
+    st[1 + f] = mean;
+    st[1 + F + f] = Q;
   }
 }
 
@@ -694,7 +790,7 @@ int mw_lognorm(const void* d_img, int dtype, int64_t n_pix, int C, const float* 
 }
 
 size_t mw_blur_ws_bytes(int H, int W, int C, int radius) {
-  return radius > kRingMax ? (size_t)H * W * C * sizeof(float) + 256 : 0;
+  return (radius > kRingMax || C % 2) ? (size_t)H * W * C * sizeof(float) + 256 : 0;
 }
 
 int mw_blur(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
@@ -767,7 +863,7 @@ size_t mw_gather_ws_bytes(int64_t S, int F) {
 int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F, const int32_t* d_idx,
                    const uint32_t* d_rank2pix, int64_t S, float* d_X, void* d_ws, void* stream) {
   MW_CHECK_ARG(d_img && d_feat && d_idx && d_rank2pix && d_X && d_ws, "mw_gather_rows: null pointer");
-  MW_CHECK_ARG(S > 0 && F > 0 && F <= 256 && C > 0, "mw_gather_rows: bad shape S=%lld F=%d",
+  MW_CHECK_ARG(S > 0 && F > 0 && F <= 64 && C > 0, "mw_gather_rows: bad shape S=%lld F=%d",
                (long long)S, F);
   hipStream_t st = as_stream(stream);
   const int G = stream_blocks(S);
@@ -782,8 +878,8 @@ int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F, cons
 
 int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats, int accumulate,
                           void* stream) {
-  MW_CHECK_ARG(d_ws && d_stats && F > 0 && F <= 1024, "mw_col_stats_finalize: bad args");
-  hipLaunchKernelGGL(col_stats_kernel, dim3(1), dim3(1024), 0, as_stream(stream),
+  MW_CHECK_ARG(d_ws && d_stats && F > 0 && F <= 64, "mw_col_stats_finalize: bad args (F <= 64)");
+  hipLaunchKernelGGL(col_stats_kernel, dim3(1), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), stream_blocks(S), F, d_stats, accumulate);
   MW_LAUNCH_CHECK();
   return MW_OK;

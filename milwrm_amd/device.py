@@ -56,6 +56,15 @@ class Workspace:
 WS = Workspace()
 
 
+def h2d(a, device=None) -> torch.Tensor:
+    """Small host array → device without a synchronous pageable copy: staged
+    through torch's caching pinned-host allocator, copied non-blocking on the
+    current stream."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return t.pin_memory().to(device if device is not None else torch.cuda.current_device(),
+                             non_blocking=True)
+
+
 def dtype_code(t: torch.Tensor) -> int:
     try:
         return _DTYPE_CODE[t.dtype]

@@ -36,10 +36,10 @@ class DeviceRows:
         self.mu = np.zeros(self.F) if mu is None else np.asarray(mu, dtype=np.float64)
         self.inv = np.ones(self.F) if inv is None else np.asarray(inv, dtype=np.float64)
         dev = X.device
-        self.mu64 = torch.from_numpy(self.mu.copy()).to(dev)
-        self.inv64 = torch.from_numpy(self.inv.copy()).to(dev)
-        self.a32 = torch.from_numpy(self.inv.astype(np.float32)).to(dev)
-        self.b32 = torch.from_numpy((-self.mu * self.inv).astype(np.float32)).to(dev)
+        self.mu64 = D.h2d(self.mu, dev)
+        self.inv64 = D.h2d(self.inv, dev)
+        self.a32 = D.h2d(self.inv.astype(np.float32), dev)
+        self.b32 = D.h2d((-self.mu * self.inv).astype(np.float32), dev)
         self._feature_var = feature_var
 
     @classmethod
@@ -158,7 +158,7 @@ def _relocate_empty(rows: DeviceRows, labels: torch.Tensor, centers_old, centers
     else:
         S, F = rows.S, rows.F
         k = centers_old.shape[0]
-        c64 = torch.from_numpy(np.ascontiguousarray(centers_old)).to(rows.X.device)
+        c64 = D.h2d(centers_old, rows.X.device)
         top_i = torch.empty(n_empty, dtype=torch.int64, device=rows.X.device)
         top_v = torch.empty(n_empty, dtype=torch.float64, device=rows.X.device)
         ws = D.WS.get("far", N.query("mw_farthest_ws_bytes", S))

@@ -34,6 +34,55 @@ def subsample_indices(M: int, fract: float, random_state: int = 16, out=None) ->
     return out
 
 
+# ---- device generator (MT19937 jump-ahead, csrc/rng.hip) -------------------
+MT_SEGMENT = 624 * 128   # words per segment
+MT_LEVELS = 24           # jump tables t^(L 2^j) mod phi, j < 24 (2^24 segments)
+_tables = {}
+
+
+def _jump_tables(device):
+    """Host-computed jump polynomials (Berlekamp-Massey + squarings, ~0.1 s,
+    once per process) uploaded to ``device``."""
+    import torch
+
+    from . import _native as N
+
+    key = str(device)
+    if key not in _tables:
+        h = np.zeros((MT_LEVELS, 312), dtype=np.uint64)
+        N.call("mw_mt_jump_tables", MT_SEGMENT, MT_LEVELS, h.ctypes.data)
+        _tables[key] = torch.from_numpy(h.view(np.int64)).to(device)
+    return _tables[key]
+
+
+def subsample_indices_device(M: int, fract: float, random_state: int = 16, device=None):
+    """Device twin of ``subsample_indices``: returns (int32 tensor of
+    int(M*fract) indices, int64 device tensor with the number of accepted
+    draws produced, to be checked >= S after the next synchronisation)."""
+    import torch
+
+    from . import _native as N
+    from . import device as D
+
+    dev = device if device is not None else D.device()
+    S = int(M * fract)
+    out = torch.empty(S, dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    if S == 0:
+        return out, total
+    if M > 2**31:
+        raise NotImplementedError("subsample over more than 2^31 masked pixels")
+    ws = D.WS.get("mtrng", N.query("mw_legacy_randint_ws_bytes", int(M), S, MT_SEGMENT))
+    N.call("mw_legacy_randint_device", int(random_state) & 0xFFFFFFFF, int(M), S,
+           D.P(_jump_tables(dev)), MT_LEVELS, MT_SEGMENT, D.P(out), D.P(total), D.P(ws), D.stream())
+    return out, total
+
+
+def check_total(total, S: int):
+    if S and int(total.item()) < S:  # pragma: no cover - 16-sigma margin
+        raise RuntimeError("device MT19937 produced too few accepted draws; increase the margin")
+
+
 def as_random_state(random_state):
     """sklearn ``check_random_state`` semantics."""
     if random_state is None or random_state is np.random:

@@ -113,3 +113,34 @@ def test_scaler_constant_feature_rule():
     st = np.concatenate([[10.0], X.mean(0), X.var(0) * 10])
     s2 = StandardScaler.from_stats(st)
     np.testing.assert_allclose(s2.scale_, s.scale_)
+
+
+def test_mt_jump_tables_and_host_jump_match_sequential_stream():
+    """phi from Berlekamp-Massey + t^(L 2^j) mod phi: jumping the seeded
+    window by L*2^j equals advancing the generator sequentially."""
+    from milwrm_amd import _native as N
+    from oracle.milwrm_oracle import mt19937_init
+
+    L, J = 624 * 3, 3
+    tab = np.zeros((J, 312), dtype=np.uint64)
+    N.call("mw_mt_jump_tables", L, J, tab.ctypes.data)
+    st0 = np.zeros(624, dtype=np.uint32)
+    N.call("mw_mt_seed_state", 16, st0.ctypes.data)
+    np.testing.assert_array_equal(st0, mt19937_init(16))
+
+    def regen(mt):
+        mt = mt.astype(np.uint64).copy()
+        for i in range(624):
+            y = (int(mt[i]) & 0x80000000) | (int(mt[(i + 1) % 624]) & 0x7FFFFFFF)
+            mt[i] = int(mt[(i + 397) % 624]) ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+        return mt.astype(np.uint32)
+
+    wins = [st0]
+    for _ in range(12):
+        wins.append(regen(wins[-1]))
+    for j in range(J):
+        out = np.zeros(624, dtype=np.uint32)
+        N.call("mw_mt_jump_host", st0.ctypes.data, tab[j].ctypes.data, out.ctypes.data)
+        ref = wins[(L << j) // 624]
+        np.testing.assert_array_equal(out[1:], ref[1:])
+        assert (out[0] >> 31) == (ref[0] >> 31)

@@ -283,3 +283,20 @@ def test_large_properties(gpu):
         sel_j = L == j
         assert dm[8 + j] == sel_j.sum()
         np.testing.assert_allclose(dm[j], np.nansum(Cf[sel_j].astype(np.float64)), rtol=1e-6)
+
+
+def test_device_mt19937_subsample_indices_bit_exact(gpu):
+    from milwrm_amd.rng import subsample_indices_device
+
+    for M, fr in [(6540, 0.2), (1, 0.9), (2, 0.5), (1000, 0.5), (2**20, 0.01), (2**20 + 1, 0.3),
+                  (123457, 0.3), (2**31 - 1, 1e-5), (85_000_000, 0.2)]:
+        np.random.seed(16)
+        ref = np.random.choice(M, int(M * fr))
+        got, tot = subsample_indices_device(M, fr, 16)
+        assert int(tot.item()) >= ref.shape[0]
+        np.testing.assert_array_equal(got.cpu().numpy(), ref, err_msg=f"M={M}")
+    for seed in (0, 18, 2**32 - 1):
+        np.random.seed(seed)
+        ref = np.random.choice(777_777, 300_000)
+        got, _ = subsample_indices_device(777_777, 300_000 / 777_777 + 1e-12, seed)
+        np.testing.assert_array_equal(got.cpu().numpy(), ref)
