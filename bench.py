@@ -15,6 +15,7 @@ Prints ONE JSON line (rank 0).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -52,6 +53,10 @@ def make_step(raw, mask, k, comm):
     import milwrm_amd as M
 
     def step():
+        with contextlib.redirect_stdout(sys.stderr):  # reference-style progress prints
+            return _step()
+
+    def _step():
         im = M.img.from_device(raw, mask)
         est, pix = im.calculate_non_zero_mean()
         est, pix = comm.batch_stats(est, pix)

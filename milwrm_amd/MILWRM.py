@@ -264,6 +264,21 @@ class mxif_labeler(tissue_labeler):
             raise Exception("Img column in the dataframe should be either str for paths to the "
                             "files or mxif.img object")
 
+    @property
+    def merged_batch_labels(self):
+        """MILWRM.py:1734-1737: image index of every clustering row (a plain
+        list, built lazily — it has S entries and only the UMAP plots read it)."""
+        if getattr(self, "_mbl", None) is None:
+            counts = getattr(self, "_batch_counts", None)
+            if counts is None:
+                raise AttributeError("merged_batch_labels")
+            self._mbl = list(itertools.chain(*[[x] * c for x, c in enumerate(counts)]))
+        return self._mbl
+
+    @merged_batch_labels.setter
+    def merged_batch_labels(self, value):
+        self._mbl = value
+
     def _batch_means(self, comm=LOCAL_COMM):
         """MILWRM.py:1706-1714 (summed over ranks when sharded)."""
         per = {}
@@ -283,6 +298,7 @@ class mxif_labeler(tissue_labeler):
         statistics are merged across ranks."""
         comm = LOCAL_COMM if comm is None else comm
         self._comm = comm
+        self._mbl = None
         if self._rows is not None or self._cluster_host is not None:
             print("WARNING: overwriting existing cluster data")
             self.cluster_data = None
@@ -323,7 +339,7 @@ class mxif_labeler(tissue_labeler):
             off += S
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))
-        self.merged_batch_labels = list(itertools.chain(*[[x] * c for x, c in enumerate(counts)]))
+        self._batch_counts = counts  # merged_batch_labels is built on first access
         if use_path:
             self.image_df["Img"] = paths
         else:

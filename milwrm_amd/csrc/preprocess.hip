@@ -50,7 +50,7 @@ __device__ __forceinline__ float lognorm1(float x, float inv, float p) {
   const float v = t + p;
   const float e = (v - p) - t;  // rounding error of t + p (exact)
   const float l2 = __builtin_amdgcn_logf(v);  // log2, 1 ulp
-  return l2 * 0.30102999566398120f - (e / v) * 0.43429448190325182f;
+  return l2 * 0.30102999566398120f - (e * __builtin_amdgcn_rcpf(v)) * 0.43429448190325182f;
 }
 
 template <typename T> struct VecOf;
@@ -196,9 +196,10 @@ __global__ void lognorm_kernel(const T* __restrict__ img, int64_t n_elem, int C,
 constexpr int kMaxRadius = 32;
 struct BlurTaps { float w[2 * kMaxRadius + 1]; };
 
-constexpr int kPPT = 2;     // output element PAIRS per thread per row
-constexpr int kMaxL = 8;    // input-row pair loads per thread per row (static bound)
+constexpr int kMaxL = 3;    // input-row pair loads per thread per row (static bound)
 constexpr int kBlurBH = 256;
+
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 template <typename T> struct Pair2;
 template <> struct Pair2<uint8_t> { using type = uchar2; };
@@ -206,8 +207,9 @@ template <> struct Pair2<uint16_t> { using type = ushort2; };
 template <> struct Pair2<float> { using type = float2; };
 
 // Requires C even: element pairs (2p, 2p+1) never straddle a pixel, so every
-// LDS / global access below is an aligned 8-byte (fp32) or 2-element load and
-// consecutive lanes touch consecutive pairs (conflict-free ds_read_b64).
+// LDS / global access is an aligned 2-element access and consecutive lanes
+// touch consecutive pairs (conflict-free ds_read_b64).  One output pair per
+// thread; input rows are prefetched two rows ahead into registers.
 template <typename T, int R>
 __global__ void __launch_bounds__(1024) blur_kernel(const T* __restrict__ in, int H, int W, int C, int BW,
                                                     const float* __restrict__ inv_mean, float pseudo,
@@ -225,105 +227,91 @@ __global__ void __launch_bounds__(1024) blur_kernel(const T* __restrict__ in, in
   const int rowcap = (BW + 2 * R) * C;
   const int nrows = (y1 - y0) + 2 * R;
   const bool logn = inv_mean != nullptr;
-  const int npairs = bw * C / 2;
 
-  // output pairs p = t + i*nt (strided: lanes read/write consecutive pairs)
-  int e_pos[kPPT];
-  bool e_ok[kPPT];
-#pragma unroll
-  for (int i = 0; i < kPPT; ++i) {
-    const int p = t + i * nt;
-    e_ok[i] = p < npairs;
-    e_pos[i] = e_ok[i] ? 2 * p : 0;
-  }
-  // input load slots (pairs), fixed for every row
+  const bool e_ok = t < bw * C / 2;
+  const int e_pos = e_ok ? 2 * t : 0;
+  // input load slots (pairs), fixed for every row; unused slots load pair 0
   int l_src[kMaxL];
-  float2 l_inv[kMaxL];
+  bool l_ok[kMaxL];
+  f2v l_inv[kMaxL];
 #pragma unroll
   for (int k = 0; k < kMaxL; ++k) {
-    const int q = t + k * nt;  // pair index in the halo'd row
-    l_src[k] = -1;
-    l_inv[k] = make_float2(1.f, 1.f);
-    if (q < seg2) {
+    const int q = t + k * nt;
+    l_ok[k] = q < seg2;
+    l_src[k] = 0;
+    l_inv[k] = f2v{1.f, 1.f};
+    if (l_ok[k]) {
       const int e = 2 * q;
       const int px = e / C;
       const int c = e - px * C;
       int gx = x0 - R + px;
       gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
       l_src[k] = gx * C + c;
-      if (logn) l_inv[k] = make_float2(inv_mean[c], inv_mean[c + 1]);
+      if (logn) l_inv[k] = f2v{inv_mean[c], inv_mean[c + 1]};
     }
   }
-  float2 ring[kPPT][NR];
+  f2v wv[NR];
 #pragma unroll
-  for (int i = 0; i < kPPT; ++i)
+  for (int j = 0; j < NR; ++j) wv[j] = f2v{taps.w[j], taps.w[j]};
+  f2v ring[NR];
 #pragma unroll
-    for (int j = 0; j < NR; ++j) ring[i][j] = make_float2(0.f, 0.f);
+  for (int j = 0; j < NR; ++j) ring[j] = f2v{0.f, 0.f};
 
-  float2 pre[kMaxL];
-  auto fetch_row = [&](int rr) {
+  P2 pa[kMaxL], pb[kMaxL];  // raw prefetch registers: rows rr+1 (pa) and rr+2 (pb)
+  auto fetch_row = [&](int rr, P2 (&dst)[kMaxL]) {
     int yy = y0 - R + rr;
     yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
+    yy = rr < nrows ? yy : y0;  // past the end: harmless re-read
     const T* src = in + (int64_t)yy * W * C;
 #pragma unroll
-    for (int k = 0; k < kMaxL; ++k) {
-      const P2 v = *reinterpret_cast<const P2*>(src + (l_src[k] >= 0 ? l_src[k] : 0));
-      pre[k] = make_float2((float)v.x, (float)v.y);
-    }
+    for (int k = 0; k < kMaxL; ++k) dst[k] = *reinterpret_cast<const P2*>(src + l_src[k]);
   };
-  auto store_row = [&](int buf) {
-    float2* dst = reinterpret_cast<float2*>(s_row + buf * rowcap);
+  auto store_row = [&](int buf, const P2 (&v)[kMaxL]) {
+    f2v* dst = reinterpret_cast<f2v*>(s_row + buf * rowcap);
 #pragma unroll
     for (int k = 0; k < kMaxL; ++k) {
-      if (l_src[k] >= 0) {
-        float2 v = pre[k];
+      if (l_ok[k]) {
+        f2v x = f2v{(float)v[k].x, (float)v[k].y};
         if (logn) {
-          v.x = lognorm1(v.x, l_inv[k].x, pseudo);
-          v.y = lognorm1(v.y, l_inv[k].y, pseudo);
+          x.x = lognorm1(x.x, l_inv[k].x, pseudo);
+          x.y = lognorm1(x.y, l_inv[k].y, pseudo);
         }
-        dst[t + k * nt] = v;
+        dst[t + k * nt] = x;
       }
     }
   };
 
-  fetch_row(0);
-  store_row(0);
+  fetch_row(0, pa);
+  fetch_row(1, pb);
+  store_row(0, pa);
+#pragma unroll
+  for (int k = 0; k < kMaxL; ++k) pa[k] = pb[k];  // pa = row 1
+  fetch_row(2, pb);                                // pb = row 2
   __syncthreads();
   for (int base = 0; base < nrows; base += NR) {
 #pragma unroll
     for (int s = 0; s < NR; ++s) {
       const int rr = base + s;
       if (rr < nrows) {
-        const bool more = rr + 1 < nrows;
-        if (more) fetch_row(rr + 1);  // global loads in flight during the compute
-        const float* row = s_row + (rr & 1) * rowcap;
+        const f2v* row = reinterpret_cast<const f2v*>(s_row + (rr & 1) * rowcap);
+        f2v h = f2v{0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < kPPT; ++i) {
-          float2 h = make_float2(0.f, 0.f);
-#pragma unroll
-          for (int j = 0; j < NR; ++j) {
-            const float2 v = *reinterpret_cast<const float2*>(row + e_pos[i] + j * C);
-            h.x = fmaf(taps.w[j], v.x, h.x);
-            h.y = fmaf(taps.w[j], v.y, h.y);
-          }
-          ring[i][s] = h;
-        }
+        for (int j = 0; j < NR; ++j)
+          h = __builtin_elementwise_fma(wv[j], row[(e_pos >> 1) + j * (C >> 1)], h);
+        ring[s] = h;
         if (rr >= 2 * R) {
-          const int y = y0 + rr - 2 * R;
-          float* orow = out + ((int64_t)y * W + x0) * C;
+          f2v v = f2v{0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < kPPT; ++i) {
-            float2 v = make_float2(0.f, 0.f);
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {
-              const float2 r2 = ring[i][(s + 1 + j) % NR];
-              v.x = fmaf(taps.w[j], r2.x, v.x);
-              v.y = fmaf(taps.w[j], r2.y, v.y);
-            }
-            if (e_ok[i]) *reinterpret_cast<float2*>(orow + e_pos[i]) = v;
+          for (int j = 0; j < NR; ++j) v = __builtin_elementwise_fma(wv[j], ring[(s + 1 + j) % NR], v);
+          if (e_ok) {
+            const int y = y0 + rr - 2 * R;
+            *reinterpret_cast<f2v*>(out + ((int64_t)y * W + x0) * C + e_pos) = v;
           }
         }
-        if (more) store_row((rr + 1) & 1);
+        if (rr + 1 < nrows) store_row((rr + 1) & 1, pa);  // row rr+1 (loaded 2 rows ago)
+#pragma unroll
+        for (int k = 0; k < kMaxL; ++k) pa[k] = pb[k];
+        fetch_row(rr + 3, pb);  // keep two rows in flight
         __syncthreads();
       }
     }
@@ -333,14 +321,17 @@ __global__ void __launch_bounds__(1024) blur_kernel(const T* __restrict__ in, in
 template <typename T, int R>
 static int launch_blur_r(const T* in, int H, int W, int C, const float* inv_mean, float p,
                          const BlurTaps& taps, float* out, hipStream_t st) {
-  int BW = 64;
-  while (BW > 1 && (BW * C / 2 + kPPT - 1) / kPPT > 1024) BW >>= 1;
-  int nt = (BW * C / 2 + kPPT - 1) / kPPT;
-  nt = ((nt + 63) / 64) * 64;
+  // one output pair per thread: BW * C / 2 <= 1024 threads
+  int BW = 128;
+  while (BW > 1 && BW * C / 2 > 1024) BW >>= 1;
+  int nt = ((BW * C / 2 + 63) / 64) * 64;
   MW_CHECK_ARG(nt <= 1024, "mw_blur: C=%d too large", C);
   const size_t lds = 2 * (size_t)(BW + 2 * R) * C * sizeof(float);
   MW_CHECK_ARG(lds <= 160 * 1024, "mw_blur: LDS %zu too large (C=%d, r=%d)", lds, C, R);
-  MW_CHECK_ARG((BW + 2 * R) * C / 2 <= kMaxL * nt, "mw_blur: row segment exceeds load slots (C=%d r=%d)", C, R);
+  if ((BW + 2 * R) * C / 2 > kMaxL * nt) {
+    set_error("mw_blur: row segment exceeds load slots (C=%d r=%d)", C, R);
+    return MW_EUNSUPPORTED;
+  }
   dim3 grid((W + BW - 1) / BW, (H + kBlurBH - 1) / kBlurBH);
   hipLaunchKernelGGL((blur_kernel<T, R>), grid, dim3(nt), lds, st, in, H, W, C, BW, inv_mean, p,
                      taps, out);
