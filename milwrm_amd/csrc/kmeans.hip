@@ -32,27 +32,24 @@ static inline int64_t krows(int64_t n) {
   return ((tiles + g - 1) / g) * kT;
 }
 
-// coalesced copy of `n` consecutive floats into LDS: 16-B vectors issued in
-// batches of 8 per thread (all loads in flight before the first LDS store),
-// then the tail.
-__device__ __forceinline__ void stage(const float* __restrict__ src, int n, float* dst) {
-  const int n4 = n >> 2;
-  const float4* s4 = reinterpret_cast<const float4*>(src);
-  float4* d4 = reinterpret_cast<float4*>(dst);
-  const int nt = blockDim.x;
-  for (int q0 = threadIdx.x; q0 < n4; q0 += 8 * nt) {
-    float4 r[8];
-    // unconditional loads from clamped (valid) addresses: a guarded load makes
-    // hipcc branch around it and wait vmcnt(0) per element
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] = s4[min(q0 + i * nt, n4 - 1)];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int q = q0 + i * nt;
-      if (q < n4) d4[q] = r[i];
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// ---- wave tiles: 64 consecutive rows of F floats (64*F floats, float4-aligned
+// because tile starts are multiples of 64 rows).  Each lane fetches NV =
+// FMAX/4 float4 with clamped, unconditional loads (guide §5.4c) and stores all
+// of them to the wave's LDS tile of 64*FMAX floats: floats past 64*F are the
+// following rows' data, read by the E-step only for padded features whose scale
+// is exactly 0.  Floats past the array's last whole float4 are patched with
+// scalar loads in the final tile only.
+__device__ __forceinline__ void wt_tail(int nfl, int64_t e0, int64_t n4, const float* __restrict__ X,
+                                        int64_t total, float* s, int lane) {
+  if (e0 + nfl > n4 * 4) {  // wave-uniform
+    for (int e = lane; e < nfl; e += 64) {
+      const int64_t ge = e0 + e;
+      if (ge >= n4 * 4 && ge < total) s[e] = X[ge];
     }
   }
-  for (int q = (n4 << 2) + threadIdx.x; q < n; q += nt) dst[q] = src[q];
 }
 
 // ===================================================================== kpp
@@ -85,43 +82,6 @@ __device__ __host__ inline KppState kpp_state(char* base, const KppLayout& L, in
   s.chosen = s.cand + T;
   s.best = reinterpret_cast<int*>(s.chosen + 256);
   return s;
-}
-
-// distance of every row to one center row (fp64), block sums.  Writes
-// bank[0][0][:] and bsum[0][0][:].
-__global__ void __launch_bounds__(256) kpp_init_kernel(const float* __restrict__ X, int64_t S, int F,
-                                                       const double* __restrict__ mu,
-                                                       const double* __restrict__ inv,
-                                                       const float* __restrict__ crow,
-                                                       int64_t R, double* __restrict__ out,
-                                                       double* __restrict__ bsum,
-                                                       int64_t* __restrict__ chosen) {
-  extern __shared__ __attribute__((aligned(16))) float s_tile[];
-  __shared__ double s_c[256];
-  __shared__ double s_red[4];
-  const int t = threadIdx.x;
-  for (int f = t; f < F; f += 256) s_c[f] = ((double)crow[f] - mu[f]) * inv[f];
-  if (blockIdx.x == 0 && t == 0) chosen[0] = -1;  // the caller knows the first index
-  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
-  double acc = 0.0;
-  __syncthreads();
-  for (int64_t r0 = lo; r0 < hi; r0 += kT) {
-    const int nrow = (int)min((int64_t)kT, hi - r0);
-    stage(X + r0 * F, nrow * F, s_tile);
-    __syncthreads();
-    if (t < nrow) {
-      double d = 0.0;
-      for (int f = 0; f < F; ++f) {
-        const double v = ((double)s_tile[t * F + f] - mu[f]) * inv[f] - s_c[f];
-        d = fma(v, v, d);
-      }
-      out[r0 + t] = d;
-      acc += d;
-    }
-    __syncthreads();
-  }
-  const double tot = block_sum(acc, s_red);
-  if (t == 0) bsum[blockIdx.x] = tot;
 }
 
 // inclusive scan of G block sums in LDS (fixed order; shared by search and
@@ -256,68 +216,114 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(const double* __restri
   }
 }
 
-// trial pass: distances to the T candidates, elementwise min with the current
-// closest distances, per-block sums.  cur = bank_prev + best*S.
-__global__ void __launch_bounds__(256) kpp_trial_kernel(const float* __restrict__ X, int64_t S, int F,
-                                                        const double* __restrict__ mu,
-                                                        const double* __restrict__ inv,
-                                                        const double* __restrict__ bank_prev,
-                                                        const int* __restrict__ best, int best_val,
-                                                        const int64_t* __restrict__ cand,
-                                                        const float* __restrict__ cand_rows, int T,
-                                                        int64_t R, double* __restrict__ bank_new,
-                                                        double* __restrict__ bsum_new) {
-  extern __shared__ __attribute__((aligned(16))) float s_tile[];
-  __shared__ double s_c[8 * 64];
+// Distance pass of k-means++ (sklearn _kmeans_plusplus, _kmeans.py:225-260):
+// fp64 squared distances of every row to T candidate rows (scaled on the fly,
+// same FMA order as a sequential per-feature loop), elementwise min with the
+// current closest distances cur = bank_prev[best] (init: no min), written to
+// bank_new[t], plus per-block sums.  Candidate rows come from `rows`
+// (T x F floats, host-gathered or the first center) or X[cand[t]].
+// Waves stream 64-row tiles with the next tile's loads in flight (as Lloyd).
+template <int FMAX>
+__global__ void __launch_bounds__(256) kpp_dist_kernel(
+    const float* __restrict__ X, int64_t S, int F, const double* __restrict__ mu,
+    const double* __restrict__ inv, const double* __restrict__ bank_prev,
+    const int* __restrict__ best, int best_val, const int64_t* __restrict__ cand,
+    const float* __restrict__ rows, int T, int64_t R, double* __restrict__ bank_new,
+    double* __restrict__ bsum_new, int64_t* __restrict__ chosen_reset) {
+  constexpr int NV = FMAX / 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ double s_c[8 * FMAX];
+  __shared__ double s_mu[FMAX], s_inv[FMAX];
   __shared__ double s_red[4];
-  const int t = threadIdx.x;
-  for (int q = t; q < T * F; q += 256) {
-    const int k = q / F, f = q - k * F;
-    const float xv = cand_rows ? cand_rows[k * F + f] : X[cand[k] * F + f];
-    s_c[k * 64 + f] = ((double)xv - mu[f]) * inv[f];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
+  float* s_tile = reinterpret_cast<float*>(smem) + (size_t)wid * 64 * FMAX;
+  for (int f = t; f < FMAX; f += blockDim.x) {
+    s_mu[f] = f < F ? mu[f] : 0.0;  // padded features scale to exactly 0
+    s_inv[f] = f < F ? inv[f] : 0.0;
   }
-  const double* cur = bank_prev + (size_t)(best ? *best : best_val) * S;
+  for (int q = t; q < 8 * FMAX; q += blockDim.x) {
+    const int c = q / FMAX, f = q - c * FMAX;
+    double v = 0.0;
+    if (c < T && f < F) {
+      const float xv = rows ? rows[c * F + f] : X[cand[c] * F + f];
+      v = ((double)xv - mu[f]) * inv[f];
+    }
+    s_c[q] = v;
+  }
+  if (chosen_reset && blockIdx.x == 0 && t == 0) chosen_reset[0] = -1;
+  const double* cur = bank_prev ? bank_prev + (size_t)(best ? *best : best_val) * S : nullptr;
+  __syncthreads();
+
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
+  const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
+  const int64_t total = S * (int64_t)F, n4 = total >> 2;
+  const f4v* X4 = reinterpret_cast<const f4v*>(X);
   double acc[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.0;
-  __syncthreads();
-  for (int64_t r0 = lo; r0 < hi; r0 += kT) {
-    const int nrow = (int)min((int64_t)kT, hi - r0);
-    stage(X + r0 * F, nrow * F, s_tile);
-    __syncthreads();
-    if (t < nrow) {
-      const int64_t s = r0 + t;
-      const double cd = cur[s];
-      double d[8];
+  for (int c = 0; c < 8; ++c) acc[c] = 0.0;
+
+  f4v v[NV];
+  double cur_next = 0.0;
+  auto fetch = [&](int tt) {
+    tt = tt < ntile ? tt : ntile - 1;
+    const int64_t r = lo + (int64_t)tt * 64;
+    if (cur) cur_next = cur[min(r + lane, hi - 1)];
+    const int64_t q0 = (r * F) >> 2;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) d[k] = 0.0;
-      for (int f = 0; f < F; ++f) {
-        const double x = ((double)s_tile[t * F + f] - mu[f]) * inv[f];
+    for (int i = 0; i < NV; ++i) {
+      int64_t q = q0 + lane + i * 64;
+      q = q < n4 ? q : n4 - 1;
+      v[i] = X4[q];
+    }
+  };
+  int tc = wid;
+  if (tc < ntile) fetch(tc);
+  for (; tc < ntile; tc += nw) {
+    const int64_t r0 = lo + (int64_t)tc * 64;
+    const int nrow = (int)min((int64_t)64, hi - r0);
+    {
+      f4v* s4 = reinterpret_cast<f4v*>(s_tile);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (k < T) {
-            const double v = x - s_c[k * 64 + f];
-            d[k] = fma(v, v, d[k]);
-          }
+      for (int i = 0; i < NV; ++i) s4[lane + i * 64] = v[i];
+    }
+    wt_tail(nrow * F, r0 * F, n4, X, total, s_tile, lane);
+    const double cd = cur_next;
+    fetch(tc + nw);
+    // launder the LDS bases so the per-feature constants are re-read per tile
+    // instead of being pinned in registers across the loop
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const double* smu = s_mu + z;
+    const double* sinv = s_inv + z;
+    const double* sc = s_c + z;
+    double xs[FMAX];
+    const float* xr = s_tile + lane * F;
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) xs[f] = ((double)xr[f] - smu[f]) * sinv[f];
+    const bool valid = lane < nrow;
+    const int64_t row = r0 + lane;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (c < T) {
+        double d = 0.0;
+#pragma unroll
+        for (int f = 0; f < FMAX; ++f) {
+          const double w = xs[f] - sc[c * FMAX + f];
+          d = fma(w, w, d);
         }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if (k < T) {
-          const double m = d[k] < cd ? d[k] : cd;
-          bank_new[(size_t)k * S + s] = m;
-          acc[k] += m;
+        const double m = (cur && cd < d) ? cd : d;
+        if (valid) {
+          bank_new[(size_t)c * S + row] = m;
+          acc[c] += m;
         }
       }
     }
-    __syncthreads();
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (k < T) {
-      const double tot = block_sum(acc[k], s_red);
-      if (t == 0) bsum_new[(size_t)k * gridDim.x + blockIdx.x] = tot;
+  for (int c = 0; c < 8; ++c) {
+    if (c < T) {
+      const double tot = block_sum(acc[c], s_red);
+      if (t == 0) bsum_new[(size_t)c * gridDim.x + blockIdx.x] = tot;
     }
   }
 }
@@ -326,172 +332,218 @@ __global__ void __launch_bounds__(256) kpp_trial_kernel(const float* __restrict_
 // Per-block record: [sums k*F | counts k | changed | inertia] (fp64).
 __host__ __device__ inline int lloyd_rec(int k, int F) { return k * F + k + 2; }
 
-template <int FMAX>
+
+// bytes of one wave's LDS region: row tile [64*FMAX] | labels [64]
+__host__ __device__ inline size_t lloyd_wave_bytes(int FMAX) { return (size_t)64 * FMAX * 4 + 64 * 4; }
+
+// One Lloyd pass (lloyd_iter_chunked_dense, _k_means_lloyd.pyx:23-218):
+//   mode 0: assign + relabel + per-label sums/counts (M-step partials)
+//   mode 1: assign + relabel + inertia of the new labels
+//   mode 2: inertia of the given labels (_inertia_dense, _k_means_common.pyx:94-124)
+// Every wave streams its own 64-row tiles (tile w, w+nw, ... of the block's
+// row range) with the next tile's loads in flight during the current tile's
+// work; no block barrier until the final combine.
+//   E-step: lane = row, scaled row x' = x*a + b (fp32), squared distances as
+//           two interleaved fp32 FMA chains (v_pk_fma_f32), strict argmin.
+//   M-step: per-label sums of the RAW rows as a one-hot GEMM on the f32 MFMA
+//           (v_mfma_f32_16x16x4_f32: A[label][row] = onehot, B[row][feature] =
+//           x; bit-exact fp32 FMA chain in row order), 16 labels x 16 features
+//           per accumulator, flushed into fp64 registers after every 64-row
+//           tile.  The record holds a*sum(x) + b*count = sum of scaled rows.
+template <int FMAX, int MB>
 __global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X, int64_t S, int F,
                                                     const float* __restrict__ ga,
                                                     const float* __restrict__ gb,
                                                     const float* __restrict__ gc, int k,
                                                     uint8_t* __restrict__ labels, int mode,
                                                     int64_t R, double* __restrict__ rec) {
-  // LDS carve (16-B aligned sections): tile[256*F] f32 | cent[k*FMAX] f32 |
-  // seg[256*k] f32 | acc64[k*F] f64 | sorted[256] i32 | lab[256] i32 |
-  // wcnt[4*k] i32 | base[k] i32 | cnt[k] i32
+  constexpr int NV = FMAX / 4;                   // float4 per lane per tile
+  constexpr int NB = FMAX <= 16 ? 1 : FMAX / 16;  // 16-feature MFMA column blocks
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* s_tile = reinterpret_cast<float*>(smem);
-  float* s_cent = s_tile + kT * F + ((4 - (kT * F) % 4) % 4);
-  float* s_seg = s_cent + k * FMAX;
-  double* s_acc = reinterpret_cast<double*>(s_seg + kT * k + ((kT * k) % 2));
-  int* s_sorted = reinterpret_cast<int*>(s_acc + k * F);
-  int* s_lab = s_sorted + kT;
-  int* s_wcnt = s_lab + kT;
-  int* s_base = s_wcnt + 4 * k;
-  int* s_cnt = s_base + k;
+  __shared__ __attribute__((aligned(16))) float s_a[FMAX], s_b[FMAX];
+  __shared__ long long s_wcnt[4 * 64];
   __shared__ double s_red[4];
-  __shared__ float s_a[FMAX], s_b[FMAX];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
+  float* s_cent = reinterpret_cast<float*>(smem);  // k * FMAX (zero padded)
+  const size_t cent_bytes = ((size_t)k * FMAX * 4 + 15) & ~(size_t)15;
+  double* s_blk = reinterpret_cast<double*>(smem + cent_bytes);  // k * F block sums
+  const size_t blk_bytes = ((size_t)k * F * 8 + 15) & ~(size_t)15;
+  float* s_tile = reinterpret_cast<float*>(smem + cent_bytes + blk_bytes + (size_t)wid * lloyd_wave_bytes(FMAX));
+  int* s_lab = reinterpret_cast<int*>(s_tile + 64 * FMAX);
 
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  for (int q = t; q < k * FMAX; q += kT) {
+  for (int q = t; q < k * FMAX; q += blockDim.x) {
     const int j = q / FMAX, f = q - j * FMAX;
     s_cent[q] = f < F ? gc[j * F + f] : 0.f;
   }
-  for (int f = t; f < FMAX; f += kT) {
-    s_a[f] = f < F ? ga[f] : 0.f;
+  for (int f = t; f < FMAX; f += blockDim.x) {
+    s_a[f] = f < F ? ga[f] : 0.f;  // padded features scale to exactly 0
     s_b[f] = f < F ? gb[f] : 0.f;
   }
-  for (int q = t; q < k * F; q += kT) s_acc[q] = 0.0;
-  const int nseg = kT / F;           // segments for the M-step walk
-  const int sf = t % F, sg = t / F;  // walk thread → (feature, segment)
-  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
-  double inert = 0.0;
-  long long changed = 0;
-  long long cnt_tot = 0;
+  for (int q = t; q < k * F; q += blockDim.x) s_blk[q] = 0.0;
   __syncthreads();
-  for (int64_t r0 = lo; r0 < hi; r0 += kT) {
-    const int nrow = (int)min((int64_t)kT, hi - r0);
-    stage(X + r0 * F, nrow * F, s_tile);
-    __syncthreads();
-    int lab = -1;
-    if (t < nrow) {
-      float xr[FMAX];
+
+  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
+  const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
+  const int64_t total = S * (int64_t)F, n4 = total >> 2;
+  const f4v* X4 = reinterpret_cast<const f4v*>(X);
+  const int kk = lane >> 4, jj = lane & 15;  // MFMA operand lane map
+  double inert = 0.0;
+  long long changed = 0, cnt = 0;
+  double acc64[MB][NB][4];
 #pragma unroll
-      for (int f = 0; f < FMAX; ++f)
-        xr[f] = f < F ? fmaf(s_tile[t * F + f], s_a[f], s_b[f]) : 0.f;
-      const int old = labels[r0 + t];
-      if (mode == 2) {
-        lab = old;
-        float d = 0.f;
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-        for (int f = 0; f < FMAX; ++f) {
-          const float v = xr[f] - s_cent[lab * FMAX + f];
-          d = fmaf(v, v, d);
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc64[mb][nb][r] = 0.0;
+
+  f4v v[NV];
+  int old_next = 0;
+  // fetch tile `tt` (clamped to the last tile: a harmless re-read)
+  auto fetch = [&](int tt) {
+    tt = tt < ntile ? tt : ntile - 1;
+    const int64_t r = lo + (int64_t)tt * 64;
+    old_next = labels[min(r + lane, hi - 1)];
+    const int64_t q0 = (r * F) >> 2;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int64_t q = q0 + lane + i * 64;
+      q = q < n4 ? q : n4 - 1;
+      v[i] = X4[q];
+    }
+  };
+  int tc = wid;
+  if (tc < ntile) fetch(tc);
+  for (; tc < ntile; tc += nw) {
+    const int64_t r0 = lo + (int64_t)tc * 64;
+    const int nrow = (int)min((int64_t)64, hi - r0);
+    {
+      f4v* s4 = reinterpret_cast<f4v*>(s_tile);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) s4[lane + i * 64] = v[i];
+    }
+    wt_tail(nrow * F, r0 * F, n4, X, total, s_tile, lane);
+    const int old = old_next;
+    fetch(tc + nw);  // the next tile's loads stay in flight during this tile
+    const bool valid = lane < nrow;
+    // ---- E-step ----
+    f2v x2[FMAX / 2];
+    {
+      const float* xs = s_tile + lane * F;
+      // re-read the scaler from LDS every tile instead of pinning 2*FMAX
+      // loop-invariant registers (they would spill)
+      int z = 0;
+      asm volatile("" : "+s"(z));
+      const f2v* sa = reinterpret_cast<const f2v*>(s_a) + z;
+      const f2v* sb = reinterpret_cast<const f2v*>(s_b) + z;
+#pragma unroll
+      for (int p = 0; p < FMAX / 2; ++p)
+        x2[p] = __builtin_elementwise_fma(f2v{xs[2 * p], xs[2 * p + 1]}, sa[p], sb[p]);
+    }
+    int lab;
+    float best;
+    if (mode == 2) {
+      lab = old;
+      const f2v* c2 = reinterpret_cast<const f2v*>(s_cent + lab * FMAX);
+      f2v acc = f2v{0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < FMAX / 2; ++p) {
+        const f2v d = x2[p] - c2[p];
+        acc = __builtin_elementwise_fma(d, d, acc);
+      }
+      best = acc.x + acc.y;
+    } else {
+      lab = 0;
+      best = 0.f;
+      for (int j = 0; j < k; ++j) {
+        const f2v* c2 = reinterpret_cast<const f2v*>(s_cent + j * FMAX);
+        f2v acc = f2v{0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < FMAX / 2; ++p) {
+          const f2v d = x2[p] - c2[p];
+          acc = __builtin_elementwise_fma(d, d, acc);
         }
-        inert += (double)d;
-      } else {
-        float best = 0.f;
-        for (int j = 0; j < k; ++j) {
-          float d = 0.f;
-#pragma unroll
-          for (int f = 0; f < FMAX; ++f) {
-            const float v = xr[f] - s_cent[j * FMAX + f];
-            d = fmaf(v, v, d);
-          }
-          if (j == 0 || d < best) { best = d; lab = j; }
-        }
+        const float dd = acc.x + acc.y;
+        if (j == 0 || dd < best) { best = dd; lab = j; }
+      }
+      if (valid) {
         changed += (lab != old) ? 1 : 0;
-        labels[r0 + t] = (uint8_t)lab;
-        if (mode == 1) inert += (double)best;
-        if (mode == 0) {
-#pragma unroll
-          for (int f = 0; f < FMAX; ++f)
-            if (f < F) s_tile[t * F + f] = xr[f];  // scaled row for the M-step
-        }
+        labels[r0 + lane] = (uint8_t)lab;
       }
     }
+    if (mode >= 1 && valid) inert += (double)best;
     if (mode == 0) {
-      // ---- counting sort of the tile's rows by label (wave ballots) ----
-      s_lab[t] = lab;
-      int my_rank = 0;
+      // ---- M-step partials ----
+      s_lab[lane] = valid ? lab : -1;
       for (int j = 0; j < k; ++j) {
-        const unsigned long long m = __ballot(lab == j);
-        if (lab == j) my_rank = __popcll(m & ((1ull << lane) - 1ull));
-        if (lane == 0) s_wcnt[j * 4 + wid] = __popcll(m);
+        const unsigned long long m = __ballot(valid && lab == j);
+        if (lane == j) cnt += __popcll(m);
       }
-      __syncthreads();
-      if (wid == 0) {
-        // lanes j < k (k <= 64): totals, exclusive scan over labels
-        int tot = 0;
-        if (lane < k) tot = s_wcnt[lane * 4] + s_wcnt[lane * 4 + 1] + s_wcnt[lane * 4 + 2] + s_wcnt[lane * 4 + 3];
-        int incl = tot;
+      f4v d[MB][NB];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int v = __shfl_up(incl, o, 64);
-          if (lane >= o) incl += v;
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) d[mb][nb] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int st = 0; st < 16; ++st) {  // 4 rows per MFMA k-step
+        const int r = 4 * st + kk;
+        const int L = s_lab[r];
+        float b[NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const int f = 16 * nb + jj;  // columns past F are never read back
+          b[nb] = s_tile[r * F + (f < F ? f : F - 1)];
         }
-        if (lane < k) {
-          s_base[lane] = incl - tot;
-          s_cnt[lane] = tot;
-        }
-      }
-      __syncthreads();
-      if (lab >= 0) {
-        int pos = s_base[lab] + my_rank;
-        for (int w = 0; w < wid; ++w) pos += s_wcnt[lab * 4 + w];
-        s_sorted[pos] = t;
-      }
-      __syncthreads();
-      // ---- segmented walk: thread (sf, sg) sums feature sf over sorted
-      //      positions [sg*L, (sg+1)*L), one store per label run ----
-      const int L = (nrow + nseg - 1) / nseg;
-      if (sg < nseg) {
-        const int p_lo = sg * L, p_hi = min(nrow, p_lo + L);
-        if (p_lo < p_hi) {
-          int cur = s_lab[s_sorted[p_lo]];
-          float acc = 0.f;
-          for (int p = p_lo; p < p_hi; ++p) {
-            const int row = s_sorted[p];
-            const int l = s_lab[row];
-            if (l != cur) {
-              s_seg[(sg * k + cur) * F + sf] = acc;
-              acc = 0.f;
-              cur = l;
-            }
-            acc += s_tile[row * F + sf];
-          }
-          s_seg[(sg * k + cur) * F + sf] = acc;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const float a = (L == 16 * mb + jj) ? 1.f : 0.f;
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            d[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[nb], d[mb][nb], 0, 0, 0);
         }
       }
-      __syncthreads();
-      // ---- fold segment partials into the fp64 block accumulators ----
-      for (int q = t; q < k * F; q += kT) {
-        const int j = q / F, f = q - j * F;
-        const int c = s_cnt[j];
-        if (c > 0) {
-          const int b0 = s_base[j];
-          const int g0 = b0 / L, g1 = (b0 + c - 1) / L;
-          double sd = 0.0;
-          for (int g = g0; g <= g1; ++g) sd += (double)s_seg[(g * k + j) * F + f];
-          s_acc[q] += sd;
-        }
-      }
-      __syncthreads();
-      // accumulate per-label counts into the record tail (held in registers of
-      // threads t < k across tiles)
-      if (t < k) cnt_tot += s_cnt[t];
-      __syncthreads();
-    } else {
-      __syncthreads();
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc64[mb][nb][r] += (double)d[mb][nb][r];
     }
   }
-  // ---- block record ----
-  const int rl = lloyd_rec(k, F);
-  double* out = rec + (size_t)blockIdx.x * rl;
+  // ---- block record (fixed combine order: waves in index order) ----
+  s_wcnt[wid * 64 + lane] = cnt;
   const double ch = block_sum((double)changed, s_red);
   const double in = block_sum(inert, s_red);
+  const int rl = lloyd_rec(k, F);
+  double* out = rec + (size_t)blockIdx.x * rl;
   if (mode == 0) {
-    for (int q = t; q < k * F; q += kT) out[q] = s_acc[q];
-    if (t < k) out[k * F + t] = (double)cnt_tot;
+    for (int w = 0; w < nw; ++w) {
+      if (wid == w) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int i = 16 * mb + 4 * kk + r, f = 16 * nb + jj;  // C/D lane map
+              if (i < k && f < F) s_blk[i * F + f] += acc64[mb][nb][r];
+            }
+      }
+      __syncthreads();
+    }
+    for (int q = t; q < k * F; q += blockDim.x) {
+      const int j = q / F, f = q - j * F;
+      long long n = 0;
+      for (int w = 0; w < nw; ++w) n += s_wcnt[w * 64 + j];
+      out[q] = (double)s_a[f] * s_blk[q] + (double)s_b[f] * (double)n;
+    }
+    for (int j = t; j < k; j += blockDim.x) {
+      long long n = 0;
+      for (int w = 0; w < nw; ++w) n += s_wcnt[w * 64 + j];
+      out[k * F + j] = (double)n;
+    }
   } else {
-    for (int q = t; q < k * F + k; q += kT) out[q] = 0.0;
+    for (int q = t; q < k * F + k; q += blockDim.x) out[q] = 0.0;
   }
   if (t == 0) {
     out[k * F + k] = ch;
@@ -590,8 +642,16 @@ __global__ void argmax_final_kernel(const double* __restrict__ pv, const int64_t
 }
 
 // ============================================================ assign_conf
-// Per-block record: [sum conf k | count k] (fp64).
-template <int FMAX>
+__host__ __device__ inline size_t assign_wave_bytes(int k, int CMAX) {
+  return (size_t)(k + 1) * 64 * 12 + (size_t)64 * CMAX * 4;
+}
+// KMeans.predict + estimate_confidence_score_mxif (MILWRM.py:237-277,
+// 389-450) over every pixel of an HWC image: label of the nearest center
+// (strict argmin, same packed-FMA distance as the Lloyd E-step), confidence
+// (d2 - d1) / d2 from the two smallest distances, -1 / NaN outside the mask.
+// Per-block record: [sum conf k | count k] (fp64, fixed combine order).
+// Waves stream 64-pixel tiles (64*C floats) with the next tile in flight.
+template <int CMAX>
 __global__ void __launch_bounds__(256) assign_kernel(const float* __restrict__ img, int C,
                                                      const int32_t* __restrict__ feat, int F,
                                                      const float* __restrict__ ga,
@@ -601,73 +661,124 @@ __global__ void __launch_bounds__(256) assign_kernel(const float* __restrict__ i
                                                      int64_t R, int8_t* __restrict__ lab_out,
                                                      float* __restrict__ conf_out,
                                                      double* __restrict__ rec) {
+  constexpr int NV = CMAX / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* s_tile = reinterpret_cast<float*>(smem);                       // 256*C
-  float* s_cent = s_tile + kT * C + ((4 - (kT * C) % 4) % 4);           // k*FMAX
-  double* s_wacc = reinterpret_cast<double*>(s_cent + k * FMAX + ((k * FMAX) % 2));  // 4 waves x 2k
-  __shared__ int s_feat[FMAX];
-  __shared__ float s_a[FMAX], s_b[FMAX];
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  for (int q = t; q < k * FMAX; q += kT) {
-    const int j = q / FMAX, f = q - j * FMAX;
+  __shared__ __attribute__((aligned(16))) float s_a[CMAX], s_b[CMAX];
+  __shared__ int s_feat[CMAX];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
+  float* s_cent = reinterpret_cast<float*>(smem);  // k * CMAX (zero padded)
+  const size_t cent_bytes = ((size_t)k * CMAX * 4 + 15) & ~(size_t)15;
+  // per wave: conf sums fp64 [k+1][64] | counts u32 [k+1][64] | tile [64*CMAX]
+  const size_t wslot = assign_wave_bytes(k, CMAX);
+  char* wb = smem + cent_bytes + (size_t)wid * wslot;
+  double* w_csum = reinterpret_cast<double*>(wb);
+  unsigned* w_ccnt = reinterpret_cast<unsigned*>(w_csum + (k + 1) * 64);
+  float* s_tile = reinterpret_cast<float*>(w_ccnt + (k + 1) * 64);
+  for (int q = t; q < k * CMAX; q += blockDim.x) {
+    const int j = q / CMAX, f = q - j * CMAX;
     s_cent[q] = f < F ? gc[j * F + f] : 0.f;
   }
-  for (int f = t; f < FMAX; f += kT) {
+  for (int f = t; f < CMAX; f += blockDim.x) {
     s_feat[f] = f < F ? feat[f] : 0;
     s_a[f] = f < F ? ga[f] : 0.f;
     s_b[f] = f < F ? gb[f] : 0.f;
   }
-  for (int q = t; q < 8 * k; q += kT) s_wacc[q] = 0.0;
-  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(n, lo + R);
-  __syncthreads();
-  for (int64_t p0 = lo; p0 < hi; p0 += kT) {
-    const int np = (int)min((int64_t)kT, hi - p0);
-    stage(img + p0 * C, np * C, s_tile);
-    __syncthreads();
-    int lab = -1;
-    float conf = __builtin_nanf("");
-    if (t < np) {
-      const int64_t p = p0 + t;
-      if (mask[p] != 0) {
-        float xr[FMAX];
-#pragma unroll
-        for (int f = 0; f < FMAX; ++f)
-          xr[f] = f < F ? fmaf(s_tile[t * C + s_feat[f]], s_a[f], s_b[f]) : 0.f;
-        float m1 = 0.f, m2 = __builtin_inff();
-        for (int j = 0; j < k; ++j) {
-          float d = 0.f;
-#pragma unroll
-          for (int f = 0; f < FMAX; ++f) {
-            const float v = xr[f] - s_cent[j * FMAX + f];
-            d = fmaf(v, v, d);
-          }
-          if (j == 0) { m1 = d; lab = 0; }
-          else if (d < m1) { m2 = m1; m1 = d; lab = j; }
-          else if (d < m2) { m2 = d; }
-        }
-        conf = (m2 - m1) / m2;
-      }
-      lab_out[p] = (int8_t)lab;
-      conf_out[p] = conf;
-    }
-    // per-label sum of confidences and counts (wave-private fp64 slots)
-    for (int j = 0; j < k; ++j) {
-      const bool mine = lab == j;
-      const float v = wave_sum(mine ? conf : 0.f);
-      const unsigned long long m = __ballot(mine);
-      if (lane == 0 && m) {
-        s_wacc[(wid * 2 + 0) * k + j] += (double)v;
-        s_wacc[(wid * 2 + 1) * k + j] += (double)__popcll(m);
-      }
-    }
-    __syncthreads();
+  for (int q = lane; q < (k + 1) * 64; q += 64) {
+    w_csum[q] = 0.0;
+    w_ccnt[q] = 0u;
   }
+  __syncthreads();
+
+  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(n, lo + R);
+  const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
+  const int64_t total = n * (int64_t)C, n4 = total >> 2;
+  const f4v* X4 = reinterpret_cast<const f4v*>(img);
+
+  f4v v[NV];
+  int mask_next = 0;
+  auto fetch = [&](int tt) {
+    tt = tt < ntile ? tt : ntile - 1;
+    const int64_t r = lo + (int64_t)tt * 64;
+    mask_next = mask[min(r + lane, hi - 1)];
+    const int64_t q0 = (r * C) >> 2;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int64_t q = q0 + lane + i * 64;
+      q = q < n4 ? q : n4 - 1;
+      v[i] = X4[q];
+    }
+  };
+  int tc = wid;
+  if (tc < ntile) fetch(tc);
+  for (; tc < ntile; tc += nw) {
+    const int64_t p0 = lo + (int64_t)tc * 64;
+    const int np = (int)min((int64_t)64, hi - p0);
+    {
+      f4v* s4 = reinterpret_cast<f4v*>(s_tile);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) s4[lane + i * 64] = v[i];
+    }
+    wt_tail(np * C, p0 * C, n4, img, total, s_tile, lane);
+    const int mk = mask_next;
+    fetch(tc + nw);
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const f2v* sa = reinterpret_cast<const f2v*>(s_a) + z;
+    const f2v* sb = reinterpret_cast<const f2v*>(s_b) + z;
+    const int* sf = s_feat + z;
+    const float* xs = s_tile + lane * C;
+    f2v x2[CMAX / 2];
+#pragma unroll
+    for (int p = 0; p < CMAX / 2; ++p)
+      x2[p] = __builtin_elementwise_fma(f2v{xs[sf[2 * p]], xs[sf[2 * p + 1]]}, sa[p], sb[p]);
+    float m1 = 0.f, m2 = __builtin_inff();
+    int lab = 0;
+    for (int j = 0; j < k; ++j) {
+      const f2v* c2 = reinterpret_cast<const f2v*>(s_cent + j * CMAX);
+      f2v acc = f2v{0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < CMAX / 2; ++p) {
+        const f2v d = x2[p] - c2[p];
+        acc = __builtin_elementwise_fma(d, d, acc);
+      }
+      const float dd = acc.x + acc.y;
+      if (j == 0) { m1 = dd; lab = 0; }
+      else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
+      else if (dd < m2) { m2 = dd; }
+    }
+    const bool valid = lane < np;
+    const bool in_mask = valid && mk != 0;
+    const float conf = in_mask ? (m2 - m1) / m2 : __builtin_nanf("");
+    if (!in_mask) lab = -1;
+    if (valid) {
+      lab_out[p0 + lane] = (int8_t)lab;
+      conf_out[p0 + lane] = conf;
+    }
+    // per-label sum of confidences and counts: lane-private LDS slots in a
+    // fixed order (pixels outside the mask/tile go to the sink slot k)
+    {
+      const int slot = (lab < 0 ? k : lab) * 64 + lane;
+      atomicAdd(&w_csum[slot], in_mask ? (double)conf : 0.0);
+      atomicAdd(&w_ccnt[slot], 1u);
+    }
+  }
+  __syncthreads();
   double* out = rec + (size_t)blockIdx.x * 2 * k;
-  for (int q = t; q < 2 * k; q += kT) {
-    const int which = q / k, j = q - which * k;
-    double s = 0.0;
-    for (int w = 0; w < 4; ++w) s += s_wacc[(w * 2 + which) * k + j];
-    out[q] = s;
+  for (int q = t; q < 2 * k; q += blockDim.x) {
+    const int j = q < k ? q : q - k;
+    double sacc = 0.0;
+    for (int w = 0; w < nw; ++w) {
+      const double* cs = reinterpret_cast<const double*>(smem + cent_bytes + (size_t)w * wslot);
+      const unsigned* cc = reinterpret_cast<const unsigned*>(cs + (k + 1) * 64);
+      if (q < k) {
+        for (int l = 0; l < 64; ++l) sacc += cs[j * 64 + l];
+      } else {
+        unsigned long long c = 0;
+        for (int l = 0; l < 64; ++l) c += cc[j * 64 + l];
+        sacc += (double)c;
+      }
+    }
+    out[q] = sacc;
   }
 }
 
@@ -696,17 +807,36 @@ static KppPtrs kpp_ptrs(const void* d_ws, int64_t S, int T) {
   return p;
 }
 
+// launch the distance pass with the FMAX instance for F
+static int kpp_dist_launch(const float* X, int64_t S, int F, const double* mu, const double* inv,
+                           const double* bank_prev, const int* best, int best_val,
+                           const int64_t* cand, const float* rows, int T, const KppLayout& L,
+                           double* bank_new, double* bsum_new, int64_t* chosen_reset,
+                           hipStream_t s) {
+  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
+  const size_t lds = (size_t)4 * 64 * FM * sizeof(float);
+#define MW_KD(FMV)                                                                              \
+  hipLaunchKernelGGL(kpp_dist_kernel<FMV>, dim3(L.G), dim3(256), lds, s, X, S, F, mu, inv,     \
+                     bank_prev, best, best_val, cand, rows, T, krows(S), bank_new, bsum_new,    \
+                     chosen_reset)
+  if (FM == 8) MW_KD(8);
+  else if (FM == 16) MW_KD(16);
+  else if (FM == 32) MW_KD(32);
+  else MW_KD(64);
+#undef MW_KD
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
 int mw_kpp_init(const float* d_X, int64_t S, int F, const double* d_mu, const double* d_inv,
                 const float* d_center_row, int T, void* d_ws, void* stream) {
   MW_CHECK_ARG(d_X && d_mu && d_inv && d_ws && d_center_row, "mw_kpp_init: null pointer");
-  MW_CHECK_ARG(S > 0 && F > 0 && F <= 256, "mw_kpp_init: bad shape");
+  MW_CHECK_ARG(S > 0 && F > 0 && F <= 64, "mw_kpp_init: bad shape (F <= 64)");
   MW_CHECK_ARG(T >= 1 && T <= 8, "mw_kpp_init: n_local_trials must be in [1, 8]");
   const KppPtrs p = kpp_ptrs(d_ws, S, T);
-  hipLaunchKernelGGL(kpp_init_kernel, dim3(p.L.G), dim3(256), (size_t)kT * F * sizeof(float),
-                     as_stream(stream), d_X, S, F, d_mu, d_inv, d_center_row, krows(S),
-                     p.bank_of(0, T, S), p.bsum_of(0, T), p.st.chosen);
-  MW_LAUNCH_CHECK();
-  return MW_OK;
+  return kpp_dist_launch(d_X, S, F, d_mu, d_inv, nullptr, nullptr, 0, nullptr, d_center_row, 1,
+                         p.L, p.bank_of(0, T, S), p.bsum_of(0, T), p.st.chosen,
+                         as_stream(stream));
 }
 
 int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu, const double* d_inv, int c,
@@ -725,11 +855,8 @@ int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu, const do
                      u[4], u[5], u[6], u[7], T, p.st.cand, p.st.chosen, p.st.best, -1,
                      (const double*)nullptr);
   MW_LAUNCH_CHECK();
-  hipLaunchKernelGGL(kpp_trial_kernel, dim3(p.L.G), dim3(256), (size_t)kT * F * sizeof(float), s,
-                     d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S), p.st.best, 0, p.st.cand,
-                     (const float*)nullptr, T, krows(S), p.bank_of(c, T, S), p.bsum_of(c, T));
-  MW_LAUNCH_CHECK();
-  return MW_OK;
+  return kpp_dist_launch(d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S), p.st.best, 0, p.st.cand,
+                         nullptr, T, p.L, p.bank_of(c, T, S), p.bsum_of(c, T), nullptr, s);
 }
 
 int mw_kpp_indices(const void* d_ws, int64_t S, int T, int k, int64_t* d_idx_out, void* stream) {
@@ -778,26 +905,13 @@ int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu, const d
   MW_CHECK_ARG(c >= 1 && T >= 1 && T <= 8 && F <= 64 && best >= 0 && best < (c == 1 ? 1 : T),
                "mw_kpp_trial: bad args");
   const KppPtrs p = kpp_ptrs(d_ws, S, T);
-  hipLaunchKernelGGL(kpp_trial_kernel, dim3(p.L.G), dim3(256), (size_t)kT * F * sizeof(float),
-                     as_stream(stream), d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S),
-                     (const int*)nullptr, best, (const int64_t*)nullptr, d_rows, T, krows(S),
-                     p.bank_of(c, T, S), p.bsum_of(c, T));
-  MW_LAUNCH_CHECK();
-  return MW_OK;
+  return kpp_dist_launch(d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S), nullptr, best, nullptr,
+                         d_rows, T, p.L, p.bank_of(c, T, S), p.bsum_of(c, T), nullptr,
+                         as_stream(stream));
 }
 
 size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
   return (size_t)kblocks(S) * lloyd_rec(k, F) * sizeof(double) + 256;
-}
-
-static size_t lloyd_lds(int k, int F, int FMAX) {
-  size_t b = 0;
-  b += ((size_t)kT * F + 4) * 4;   // tile
-  b += (size_t)k * FMAX * 4;       // centers
-  b += ((size_t)kT * k + 2) * 4;   // segment partials
-  b += (size_t)k * F * 8;          // fp64 accumulators
-  b += (size_t)(2 * kT + 6 * k) * 4 + 64;
-  return (b + 15) & ~(size_t)15;
 }
 
 int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
@@ -806,7 +920,7 @@ int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a, const fl
   MW_CHECK_ARG(d_X && d_a && d_b && d_centers && d_labels && d_ws, "mw_lloyd_step: null pointer");
   MW_CHECK_ARG(S > 0 && F > 0 && k >= 1, "mw_lloyd_step: bad shape");
   MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_step: bad mode");
-  if (k > 64 || F > 64 || (mode == 0 && F > kT)) {
+  if (k > 64 || F > 64) {
     set_error("mw_lloyd_step: k=%d F=%d unsupported (k <= 64, F <= 64)", k, F);
     return MW_EUNSUPPORTED;
   }
@@ -814,21 +928,23 @@ int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a, const fl
   const int G = kblocks(S);
   const int64_t R = krows(S);
   double* rec = reinterpret_cast<double*>(d_ws);
-#define MW_LL(FM)                                                                               \
-  {                                                                                             \
-    const size_t lds = lloyd_lds(k, F, FM);                                                     \
-    if (lds > 160 * 1024) {                                                                     \
-      set_error("mw_lloyd_step: LDS %zu too large (k=%d F=%d)", lds, k, F);                     \
-      return MW_EUNSUPPORTED;                                                                   \
-    }                                                                                           \
-    hipLaunchKernelGGL(lloyd_kernel<FM>, dim3(G), dim3(kT), lds, s, d_X, S, F, d_a, d_b,        \
-                       d_centers, k, d_labels, mode, R, rec);                                   \
-  }
-  if (F <= 4) MW_LL(4)
-  else if (F <= 8) MW_LL(8)
-  else if (F <= 16) MW_LL(16)
-  else if (F <= 32) MW_LL(32)
-  else MW_LL(64)
+  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
+  const int MBv = k <= 16 ? 1 : k <= 32 ? 2 : 4;
+  const size_t cent = ((size_t)k * FM * 4 + 15) & ~(size_t)15;
+  const size_t blk = ((size_t)k * F * 8 + 15) & ~(size_t)15;
+  const size_t lds = cent + blk + 4 * lloyd_wave_bytes(FM);
+#define MW_LL(FMV, MBV)                                                                        \
+  hipLaunchKernelGGL((lloyd_kernel<FMV, MBV>), dim3(G), dim3(256), lds, s, d_X, S, F, d_a,    \
+                     d_b, d_centers, k, d_labels, mode, R, rec)
+#define MW_LLF(FMV)                \
+  if (MBv == 1) MW_LL(FMV, 1);     \
+  else if (MBv == 2) MW_LL(FMV, 2); \
+  else MW_LL(FMV, 4);
+  if (FM == 8) { MW_LLF(8) }
+  else if (FM == 16) { MW_LLF(16) }
+  else if (FM == 32) { MW_LLF(32) }
+  else { MW_LLF(64) }
+#undef MW_LLF
 #undef MW_LL
   MW_LAUNCH_CHECK();
   return MW_OK;
@@ -881,29 +997,30 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
   MW_CHECK_ARG(d_img && d_feat && d_a && d_b && d_centers && d_mask && d_label && d_conf && d_ws,
                "mw_assign_conf: null pointer");
   MW_CHECK_ARG(n_pix > 0 && C > 0 && F > 0 && k >= 1, "mw_assign_conf: bad shape");
-  if (k > 127 || F > 64) {
-    set_error("mw_assign_conf: k=%d F=%d unsupported (k <= 127, F <= 64)", k, F);
+  if (k > 127 || F > C || C > 64) {
+    set_error("mw_assign_conf: k=%d C=%d F=%d unsupported (k <= 127, F <= C <= 64)", k, C, F);
     return MW_EUNSUPPORTED;
   }
   hipStream_t s = as_stream(stream);
   const int G = kblocks(n_pix);
   const int64_t R = krows(n_pix);
   double* rec = reinterpret_cast<double*>(d_ws);
-#define MW_AS(FM)                                                                               \
+#define MW_AS(CM)                                                                               \
   {                                                                                             \
-    size_t lds = ((size_t)kT * C + 4) * 4 + ((size_t)k * FM + 2) * 4 + (size_t)8 * k * 8 + 16;  \
-    lds = (lds + 15) & ~(size_t)15;                                                             \
+    const size_t cent = ((size_t)k * CM * 4 + 15) & ~(size_t)15;                                \
+    int nw = 4;                                                                                 \
+    while (nw > 1 && cent + nw * assign_wave_bytes(k, CM) > 160 * 1024) --nw;                   \
+    const size_t lds = cent + nw * assign_wave_bytes(k, CM);                                    \
     if (lds > 160 * 1024) {                                                                     \
       set_error("mw_assign_conf: LDS %zu too large (C=%d k=%d)", lds, C, k);                    \
       return MW_EUNSUPPORTED;                                                                   \
     }                                                                                           \
-    hipLaunchKernelGGL(assign_kernel<FM>, dim3(G), dim3(kT), lds, s, d_img, C, d_feat, F, d_a,  \
-                       d_b, d_centers, k, d_mask, n_pix, R, d_label, d_conf, rec);              \
+    hipLaunchKernelGGL(assign_kernel<CM>, dim3(G), dim3(64 * nw), lds, s, d_img, C, d_feat, F,  \
+                       d_a, d_b, d_centers, k, d_mask, n_pix, R, d_label, d_conf, rec);         \
   }
-  if (F <= 4) MW_AS(4)
-  else if (F <= 8) MW_AS(8)
-  else if (F <= 16) MW_AS(16)
-  else if (F <= 32) MW_AS(32)
+  if (C <= 8) MW_AS(8)
+  else if (C <= 16) MW_AS(16)
+  else if (C <= 32) MW_AS(32)
   else MW_AS(64)
 #undef MW_AS
   MW_LAUNCH_CHECK();
