@@ -1,0 +1,7 @@
+// Fast fused log-normalise + Gaussian blur instances for float input (blur.h).
+#include "blur.h"
+
+namespace mw {
+template int launch_blur_fast<float>(const float*, int, int, int, const float*, float, const BlurTaps&,
+                                    int, float*, hipStream_t);
+}  // namespace mw

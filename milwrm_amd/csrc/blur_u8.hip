@@ -1,0 +1,7 @@
+// Fast fused log-normalise + Gaussian blur instances for uint8_t input (blur.h).
+#include "blur.h"
+
+namespace mw {
+template int launch_blur_fast<uint8_t>(const uint8_t*, int, int, int, const float*, float, const BlurTaps&,
+                                    int, float*, hipStream_t);
+}  // namespace mw

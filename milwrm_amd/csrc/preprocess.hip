@@ -16,6 +16,7 @@
 #include <math.h>
 
 #include "common.h"
+#include "blur.h"
 
 namespace mw {
 
@@ -41,16 +42,6 @@ static inline int64_t rows_per_block(int64_t n) {
   int64_t tiles = (n + kTile - 1) / kTile;
   int g = stream_blocks(n);
   return ((tiles + g - 1) / g) * kTile;
-}
-
-// accurate log10(t + p) for t >= 0 (log1p-style correction of the rounding
-// of t + p, so small t keep full relative accuracy)
-__device__ __forceinline__ float lognorm1(float x, float inv, float p) {
-  const float t = x * inv;
-  const float v = t + p;
-  const float e = (v - p) - t;  // rounding error of t + p (exact)
-  const float l2 = __builtin_amdgcn_logf(v);  // log2, 1 ulp
-  return l2 * 0.30102999566398120f - (e * __builtin_amdgcn_rcpf(v)) * 0.43429448190325182f;
 }
 
 template <typename T> struct VecOf;
@@ -186,158 +177,13 @@ __global__ void lognorm_kernel(const T* __restrict__ img, int64_t n_elem, int C,
 }
 
 // --------------------------------------------------------------------- blur
-// One workgroup = a band of BW output columns x BH output rows, all C
-// channels.  Rows stream top to bottom: each input row segment (with r-pixel
-// horizontal halo, edge-clamped) is log-normalised into a double-buffered LDS
-// row, the horizontal 2r+1-tap pass reads it from LDS, and the vertical pass
-// keeps the last 2r+1 horizontally filtered rows in a register ring per
-// element (static indices: the row loop is unrolled by 2r+1).  Output rows are
-// written as contiguous HWC segments (coalesced).
-constexpr int kMaxRadius = 32;
-struct BlurTaps { float w[2 * kMaxRadius + 1]; };
-
-constexpr int kMaxL = 3;    // input-row pair loads per thread per row (static bound)
-constexpr int kBlurBH = 256;
-
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-template <typename T> struct Pair2;
-template <> struct Pair2<uint8_t> { using type = uchar2; };
-template <> struct Pair2<uint16_t> { using type = ushort2; };
-template <> struct Pair2<float> { using type = float2; };
-
-// Requires C even: element pairs (2p, 2p+1) never straddle a pixel, so every
-// LDS / global access is an aligned 2-element access and consecutive lanes
-// touch consecutive pairs (conflict-free ds_read_b64).  One output pair per
-// thread; input rows are prefetched two rows ahead into registers.
-template <typename T, int R>
-__global__ void __launch_bounds__(1024) blur_kernel(const T* __restrict__ in, int H, int W, int C, int BW,
-                                                    const float* __restrict__ inv_mean, float pseudo,
-                                                    BlurTaps taps, float* __restrict__ out) {
-  using P2 = typename Pair2<T>::type;
-  constexpr int NR = 2 * R + 1;
-  extern __shared__ __attribute__((aligned(16))) float s_row[];  // 2 x (BW+2R)*C
-  const int t = threadIdx.x;
-  const int nt = blockDim.x;
-  const int x0 = blockIdx.x * BW;
-  const int y0 = blockIdx.y * kBlurBH;
-  const int y1 = min(H, y0 + kBlurBH);
-  const int bw = min(BW, W - x0);
-  const int seg2 = (bw + 2 * R) * C / 2;  // halo'd row pairs
-  const int rowcap = (BW + 2 * R) * C;
-  const int nrows = (y1 - y0) + 2 * R;
-  const bool logn = inv_mean != nullptr;
-
-  const bool e_ok = t < bw * C / 2;
-  const int e_pos = e_ok ? 2 * t : 0;
-  // input load slots (pairs), fixed for every row; unused slots load pair 0
-  int l_src[kMaxL];
-  bool l_ok[kMaxL];
-  f2v l_inv[kMaxL];
-#pragma unroll
-  for (int k = 0; k < kMaxL; ++k) {
-    const int q = t + k * nt;
-    l_ok[k] = q < seg2;
-    l_src[k] = 0;
-    l_inv[k] = f2v{1.f, 1.f};
-    if (l_ok[k]) {
-      const int e = 2 * q;
-      const int px = e / C;
-      const int c = e - px * C;
-      int gx = x0 - R + px;
-      gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
-      l_src[k] = gx * C + c;
-      if (logn) l_inv[k] = f2v{inv_mean[c], inv_mean[c + 1]};
-    }
-  }
-  f2v wv[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) wv[j] = f2v{taps.w[j], taps.w[j]};
-  f2v ring[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) ring[j] = f2v{0.f, 0.f};
-
-  P2 pa[kMaxL], pb[kMaxL];  // raw prefetch registers: rows rr+1 (pa) and rr+2 (pb)
-  auto fetch_row = [&](int rr, P2 (&dst)[kMaxL]) {
-    int yy = y0 - R + rr;
-    yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
-    yy = rr < nrows ? yy : y0;  // past the end: harmless re-read
-    const T* src = in + (int64_t)yy * W * C;
-#pragma unroll
-    for (int k = 0; k < kMaxL; ++k) dst[k] = *reinterpret_cast<const P2*>(src + l_src[k]);
-  };
-  auto store_row = [&](int buf, const P2 (&v)[kMaxL]) {
-    f2v* dst = reinterpret_cast<f2v*>(s_row + buf * rowcap);
-#pragma unroll
-    for (int k = 0; k < kMaxL; ++k) {
-      if (l_ok[k]) {
-        f2v x = f2v{(float)v[k].x, (float)v[k].y};
-        if (logn) {
-          x.x = lognorm1(x.x, l_inv[k].x, pseudo);
-          x.y = lognorm1(x.y, l_inv[k].y, pseudo);
-        }
-        dst[t + k * nt] = x;
-      }
-    }
-  };
-
-  fetch_row(0, pa);
-  fetch_row(1, pb);
-  store_row(0, pa);
-#pragma unroll
-  for (int k = 0; k < kMaxL; ++k) pa[k] = pb[k];  // pa = row 1
-  fetch_row(2, pb);                                // pb = row 2
-  __syncthreads();
-  for (int base = 0; base < nrows; base += NR) {
-#pragma unroll
-    for (int s = 0; s < NR; ++s) {
-      const int rr = base + s;
-      if (rr < nrows) {
-        const f2v* row = reinterpret_cast<const f2v*>(s_row + (rr & 1) * rowcap);
-        f2v h = f2v{0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < NR; ++j)
-          h = __builtin_elementwise_fma(wv[j], row[(e_pos >> 1) + j * (C >> 1)], h);
-        ring[s] = h;
-        if (rr >= 2 * R) {
-          f2v v = f2v{0.f, 0.f};
-#pragma unroll
-          for (int j = 0; j < NR; ++j) v = __builtin_elementwise_fma(wv[j], ring[(s + 1 + j) % NR], v);
-          if (e_ok) {
-            const int y = y0 + rr - 2 * R;
-            *reinterpret_cast<f2v*>(out + ((int64_t)y * W + x0) * C + e_pos) = v;
-          }
-        }
-        if (rr + 1 < nrows) store_row((rr + 1) & 1, pa);  // row rr+1 (loaded 2 rows ago)
-#pragma unroll
-        for (int k = 0; k < kMaxL; ++k) pa[k] = pb[k];
-        fetch_row(rr + 3, pb);  // keep two rows in flight
-        __syncthreads();
-      }
-    }
-  }
-}
-
-template <typename T, int R>
-static int launch_blur_r(const T* in, int H, int W, int C, const float* inv_mean, float p,
-                         const BlurTaps& taps, float* out, hipStream_t st) {
-  // one output pair per thread: BW * C / 2 <= 1024 threads
-  int BW = 128;
-  while (BW > 1 && BW * C / 2 > 1024) BW >>= 1;
-  int nt = ((BW * C / 2 + 63) / 64) * 64;
-  MW_CHECK_ARG(nt <= 1024, "mw_blur: C=%d too large", C);
-  const size_t lds = 2 * (size_t)(BW + 2 * R) * C * sizeof(float);
-  MW_CHECK_ARG(lds <= 160 * 1024, "mw_blur: LDS %zu too large (C=%d, r=%d)", lds, C, R);
-  if ((BW + 2 * R) * C / 2 > kMaxL * nt) {
-    set_error("mw_blur: row segment exceeds load slots (C=%d r=%d)", C, R);
-    return MW_EUNSUPPORTED;
-  }
-  dim3 grid((W + BW - 1) / BW, (H + kBlurBH - 1) / kBlurBH);
-  hipLaunchKernelGGL((blur_kernel<T, R>), grid, dim3(nt), lds, st, in, H, W, C, BW, inv_mean, p,
-                     taps, out);
-  MW_LAUNCH_CHECK();
-  return MW_OK;
-}
+// Fast path: blur.h, instantiated per dtype in blur_{u8,u16,f32}.hip.
+extern template int launch_blur_fast<uint8_t>(const uint8_t*, int, int, int, const float*, float,
+                                              const BlurTaps&, int, float*, hipStream_t);
+extern template int launch_blur_fast<uint16_t>(const uint16_t*, int, int, int, const float*, float,
+                                               const BlurTaps&, int, float*, hipStream_t);
+extern template int launch_blur_fast<float>(const float*, int, int, int, const float*, float,
+                                            const BlurTaps&, int, float*, hipStream_t);
 
 // Generic-radius fallback (r > kRingMax): two separable passes through an fp32
 // HWC temporary.  Pass 1 (axis 0): tmp[y,x,c] = sum_j w_j f(in[clamp(y+j-r),x,c]);
@@ -383,28 +229,21 @@ __global__ void blur_axis1_kernel(const float* __restrict__ tmp, int H, int W, i
   }
 }
 
-constexpr int kRingMax = 12;
-
 template <typename T>
 static int launch_blur(const T* in, int H, int W, int C, const float* inv_mean, float p,
                        const BlurTaps& taps, int r, float* out, float* tmp, hipStream_t st) {
-  switch ((C % 2 == 0) ? r : -1) {
-#define MW_R(N) case N: return launch_blur_r<T, N>(in, H, W, C, inv_mean, p, taps, out, st);
-    MW_R(0) MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8) MW_R(9) MW_R(10)
-    MW_R(11) MW_R(12)
-#undef MW_R
-    default: {
-      MW_CHECK_ARG(tmp != nullptr, "mw_blur: radius %d needs a workspace (mw_blur_ws_bytes)", r);
-      const int64_t n = (int64_t)H * W * C;
-      const int grid = (int)std::min<int64_t>((n + 255) / 256, 16384);
-      hipLaunchKernelGGL(blur_axis0_kernel<T>, dim3(grid), dim3(256), 0, st, in, H, W, C, inv_mean,
-                         p, taps, r, tmp);
-      MW_LAUNCH_CHECK();
-      hipLaunchKernelGGL(blur_axis1_kernel, dim3(grid), dim3(256), 0, st, tmp, H, W, C, taps, r, out);
-      MW_LAUNCH_CHECK();
-      return MW_OK;
-    }
-  }
+  const int rc = launch_blur_fast<T>(in, H, W, C, inv_mean, p, taps, r, out, st);
+  if (rc != MW_EUNSUPPORTED) return rc;
+  // two-pass fallback (odd C, C > 64 or r > kBlurMaxR)
+  MW_CHECK_ARG(tmp != nullptr, "mw_blur: radius %d / C=%d needs a workspace (mw_blur_ws_bytes)", r, C);
+  const int64_t n = (int64_t)H * W * C;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 16384);
+  hipLaunchKernelGGL(blur_axis0_kernel<T>, dim3(grid), dim3(256), 0, st, in, H, W, C, inv_mean,
+                     p, taps, r, tmp);
+  MW_LAUNCH_CHECK();
+  hipLaunchKernelGGL(blur_axis1_kernel, dim3(grid), dim3(256), 0, st, tmp, H, W, C, taps, r, out);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
 }
 
 // --------------------------------------------------------------- block_mean
@@ -781,7 +620,7 @@ int mw_lognorm(const void* d_img, int dtype, int64_t n_pix, int C, const float* 
 }
 
 size_t mw_blur_ws_bytes(int H, int W, int C, int radius) {
-  return (radius > kRingMax || C % 2) ? (size_t)H * W * C * sizeof(float) + 256 : 0;
+  return (radius > kBlurMaxR || C % 2 || C > 64) ? (size_t)H * W * C * sizeof(float) + 256 : 0;
 }
 
 int mw_blur(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,

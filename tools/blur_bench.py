@@ -1,0 +1,38 @@
+"""Blur-only timing on one synthetic 30-channel uint16 slide: kernel time per
+launch (HIP events on the launch stream) for several band widths
+(MW_BLUR_BW override), plus a bitwise cross-check between the variants."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from milwrm_amd import device as D  # noqa: E402
+
+size = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+C = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+torch.cuda.set_device(0)
+raw, mask = D.synth_slide(size, size, C, seed=7, mode="hard")
+inv = torch.rand(C, device="cuda", dtype=torch.float32) * 1e-3 + 1e-4
+ref = None
+for bw in ["", "64", "32", "16"]:
+    if bw:
+        os.environ["MW_BLUR_BW"] = bw
+    else:
+        os.environ.pop("MW_BLUR_BW", None)
+    out = D.blur(raw, 2.0, inv_mean=inv)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 10
+    e0.record()
+    for _ in range(n):
+        out = D.blur(raw, 2.0, inv_mean=inv)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    gb = size * size * C * (raw.element_size() + 4) / 1e9
+    same = None if ref is None else bool(torch.equal(out, ref))
+    if ref is None:
+        ref = out.clone()
+    print(f"BW={bw or 'default'}: {ms:.3f} ms/launch, {gb / ms:.0f} GB/s algorithmic, same={same}",
+          flush=True)
