@@ -52,13 +52,18 @@ def main():
             "init_indices": np.array_equal(ref.kmeans.init_indices_, allres[0]["idx"]),
             "n_iter": ref.kmeans.n_iter_ == allres[0]["n_iter"],
             "centers": np.max(np.abs(ref.kmeans.cluster_centers_ - allres[0]["centers"])) < 1e-6,
-            "inertia": abs(ref.kmeans.inertia_ - allres[0]["inertia"]) / ref.kmeans.inertia_ < 1e-9,
+            # block partials are fp32 one-hot MFMA sums over 64-row tiles whose
+            # boundaries move with the shard offsets: fp32-rounding-level drift
+            "inertia": abs(ref.kmeans.inertia_ - allres[0]["inertia"]) / ref.kmeans.inertia_ < 1e-7,
             "same_on_ranks": all(np.array_equal(a["centers"], allres[0]["centers"]) for a in allres),
             "labels": all(np.array_equal(np.nan_to_num(ref.tissue_IDs[r], nan=-1), allres[r]["tid"])
                           for r in range(world)),
         }
         ok = all(checks.values())
-        print("dist_gpu_check", "PASS" if ok else "FAIL", checks, flush=True)
+        print("dist_gpu_check", "PASS" if ok else "FAIL", checks,
+              "inertia rel", abs(ref.kmeans.inertia_ - allres[0]["inertia"]) / ref.kmeans.inertia_,
+              "centers abs", np.max(np.abs(ref.kmeans.cluster_centers_ - allres[0]["centers"])),
+              flush=True)
     flag = [ok]
     dist.broadcast_object_list(flag, src=0)
     dist.destroy_process_group()
