@@ -14,7 +14,7 @@ import threading
 import torch  # noqa: F401  (must precede the library load: one HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmilwrm_amd.so")
+LIB_PATH = os.environ.get("MW_LIB") or os.path.join(_HERE, "libmilwrm_amd.so")  # MW_LIB: tools only
 
 MW_U8, MW_U16, MW_F32 = 0, 1, 2
 _EINVAL, _EHIP, _EUNSUP = -1, -2, -3

@@ -15,12 +15,12 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(ROOT, "build")
-LIB = os.path.join(HERE, "libmilwrm_amd.so")
+BUILD = os.environ.get("MW_BUILD_DIR") or os.path.join(ROOT, "build")
+LIB = os.environ.get("MW_LIB") or os.path.join(HERE, "libmilwrm_amd.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MW_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
-         "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
+         "-Wno-unused-variable", "-Wno-unused-but-set-variable"] + os.environ.get("MW_EXTRA_FLAGS", "").split()
 
 
 def _sources():

@@ -13,18 +13,38 @@
 // fp64 records, fixed-order combine.  Labels: lowest index wins ties (strict
 // '<'), as the reference's argmin.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.h"
 
 namespace mw {
 
+#ifndef MW_LLOYD_WPS
+#define MW_LLOYD_WPS 1
+#endif
+#ifndef MW_ASSIGN_WPS
+#define MW_ASSIGN_WPS 1
+#endif
+#ifndef MW_KPP_WPS
+#define MW_KPP_WPS 1
+#endif
+
 constexpr int kT = 256;          // rows per tile = threads per block
 constexpr int kMaxG = 1024;
 
+static inline int kmax_grid() {
+  static int g = [] {
+    const char* e = getenv("MW_KBLOCKS");  // tuning override (<= kMaxG)
+    const int v = e ? atoi(e) : 0;
+    return (v >= 1 && v <= kMaxG) ? v : kMaxG;
+  }();
+  return g;
+}
 static inline int kblocks(int64_t n) {
   int64_t tiles = (n + kT - 1) / kT;
   if (tiles < 1) tiles = 1;
-  return (int)(tiles < kMaxG ? tiles : kMaxG);
+  const int gm = kmax_grid();
+  return (int)(tiles < gm ? tiles : gm);
 }
 static inline int64_t krows(int64_t n) {
   int64_t tiles = (n + kT - 1) / kT;
@@ -34,6 +54,7 @@ static inline int64_t krows(int64_t n) {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+__host__ __device__ constexpr int kpad4(int k) { return (k + 3) & ~3; }
 
 // ---- wave tiles: 64 consecutive rows of F floats (64*F floats, float4-aligned
 // because tile starts are multiples of 64 rows).  Each lane fetches NV =
@@ -224,7 +245,7 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(const double* __restri
 // (T x F floats, host-gathered or the first center) or X[cand[t]].
 // Waves stream 64-row tiles with the next tile's loads in flight (as Lloyd).
 template <int FMAX>
-__global__ void __launch_bounds__(256) kpp_dist_kernel(
+__global__ void __launch_bounds__(256, MW_KPP_WPS) kpp_dist_kernel(
     const float* __restrict__ X, int64_t S, int F, const double* __restrict__ mu,
     const double* __restrict__ inv, const double* __restrict__ bank_prev,
     const int* __restrict__ best, int best_val, const int64_t* __restrict__ cand,
@@ -328,6 +349,149 @@ __global__ void __launch_bounds__(256) kpp_dist_kernel(
   }
 }
 
+// ---- E-step center stream, written as inline asm so that the schedule is
+// the one below (hipcc otherwise hoists every center read of the block, 128+
+// VGPRs, and serialises the four distance chains).  hipcc does not count asm
+// memory operations in its s_waitcnt bookkeeping, so the stream waits itself
+// with counted lgkmcnt: LDS returns in order, and any LDS op the compiler
+// places in between only makes a counted wait stricter.
+template <int OFF>
+__device__ __forceinline__ f2v ds_read8(uint32_t addr) {
+  f2v r;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait4(f2v (&c)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  asm volatile("" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]));  // uses stay below the wait
+}
+// acc[q] += (x - c[q])^2 for four centers, packed over a feature pair: the four
+// subtractions then the four FMAs (no dependent pair back to back)
+__device__ __forceinline__ void dist4(f2v x, const f2v (&c)[4], f2v (&acc)[4]) {
+  f2v d0, d1, d2, d3;
+  asm volatile(
+      "v_pk_add_f32 %0, %8, %9 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_add_f32 %1, %8, %10 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_add_f32 %2, %8, %11 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_add_f32 %3, %8, %12 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %4, %0, %0, %4\n\t"
+      "v_pk_fma_f32 %5, %1, %1, %5\n\t"
+      "v_pk_fma_f32 %6, %2, %2, %6\n\t"
+      "v_pk_fma_f32 %7, %3, %3, %7"
+      : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]),
+        "+v"(acc[3])
+      : "v"(x), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]));
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
+}
+
+// Nearest center (strict '<': the lowest index wins exact ties, as the
+// reference's argmin) and, with TOP2, the second smallest distance.  Squared
+// distances of the scaled row x2 to every center; the centers sit in LDS
+// pair-major with a fixed center stride KS (cT[p * KS + j] = features 2p, 2p+1
+// of center j; zero past k), so each read is a broadcast ds_read_b64 at an
+// immediate offset.  Four centers per pass keep four independent packed-FMA
+// chains; center pairs stream kAhead pairs ahead of their FMAs.  Each center's
+// chain (even features in .x, odd in .y, then .x + .y) is the same fp32
+// operation sequence as a one-center loop, so the result does not depend on
+// the blocking.
+constexpr int kAhead = 3;
+template <int NP, int KS, int P>
+__device__ __forceinline__ void nc_read(uint32_t base, f2v (&c)[4]) {
+  c[0] = ds_read8<P * KS * 8>(base);
+  c[1] = ds_read8<P * KS * 8 + 8>(base);
+  c[2] = ds_read8<P * KS * 8 + 16>(base);
+  c[3] = ds_read8<P * KS * 8 + 24>(base);
+}
+template <int NP, int KS, int P>
+__device__ __forceinline__ void nc_pairs(uint32_t base, const f2v* x2, f2v (*c)[4], f2v (&acc)[4]) {
+  if constexpr (P < NP) {
+    if constexpr (P + kAhead < NP) nc_read<NP, KS, P + kAhead>(base, c[(P + kAhead) % (kAhead + 1)]);
+    constexpr int after = 4 * ((P + kAhead < NP) ? kAhead : (NP - 1 - P));
+    lgkm_wait4<after>(c[P % (kAhead + 1)]);
+    dist4(x2[P], c[P % (kAhead + 1)], acc);
+    nc_pairs<NP, KS, P + 1>(base, x2, c, acc);
+  }
+}
+template <int NP, int KS, int P>
+__device__ __forceinline__ void nc_prologue(uint32_t base, f2v (*c)[4]) {
+  if constexpr (P < kAhead && P < NP) {
+    nc_read<NP, KS, P>(base, c[P]);
+    nc_prologue<NP, KS, P + 1>(base, c);
+  }
+}
+template <int FMAX, int KS, bool TOP2>
+__device__ __forceinline__ void nearest_centers(const f2v (&x2)[FMAX / 2], const f2v* cT, int k,
+                                                int& lab, float& m1, float& m2) {
+  constexpr int NP = FMAX / 2;
+  const uint32_t a0 = lds_addr(cT);
+  lab = 0;
+  m1 = 0.f;
+  m2 = __builtin_inff();
+  for (int j0 = 0; j0 < k; j0 += 4) {
+    const uint32_t base = a0 + (uint32_t)j0 * 8u;
+    f2v c[kAhead + 1][4];  // register ring of center pairs in flight
+    f2v acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f2v{0.f, 0.f};
+    nc_prologue<NP, KS, 0>(base, c);
+    nc_pairs<NP, KS, 0>(base, x2, c, acc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + q;
+      if (j < k) {
+        const float dd = acc[q].x + acc[q].y;
+        if (TOP2) {
+          if (j == 0) { m1 = dd; lab = 0; }
+          else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
+          else if (dd < m2) { m2 = dd; }
+        } else if (j == 0 || dd < m1) {
+          m1 = dd;
+          lab = j;
+        }
+      }
+    }
+  }
+}
+
+// centers (k x F row-major, global) -> pair-major LDS image cT (see above)
+template <int FMAX, int KS>
+__device__ __forceinline__ void load_centers_T(const float* __restrict__ gc, int k, int F, f2v* cT) {
+  for (int q = threadIdx.x; q < (FMAX / 2) * KS; q += blockDim.x) {
+    const int p = q / KS, j = q - p * KS;
+    const int f0 = 2 * p, f1 = 2 * p + 1;
+    cT[q] = f2v{(j < k && f0 < F) ? gc[j * F + f0] : 0.f, (j < k && f1 < F) ? gc[j * F + f1] : 0.f};
+  }
+}
+
+// the lane's row of a 64-row LDS tile (row stride F floats), scaled x*a + b;
+// features past F scale to exactly 0 (a = b = 0 there)
+template <int FMAX>
+__device__ __forceinline__ void load_scaled_row(const float* s_tile, int lane, int F, const float* sa_,
+                                                const float* sb_, f2v (&x2)[FMAX / 2]) {
+  int z = 0;
+  asm volatile("" : "+s"(z));  // re-read the scaler from LDS each tile (no pinned registers)
+  const f2v* sa = reinterpret_cast<const f2v*>(sa_) + z;
+  const f2v* sb = reinterpret_cast<const f2v*>(sb_) + z;
+  const float* xs = s_tile + lane * F;
+  if ((F & 1) == 0) {  // 8-byte aligned rows: ds_read_b64 pairs
+    const f2v* xp = reinterpret_cast<const f2v*>(__builtin_assume_aligned(xs, 8));
+#pragma unroll
+    for (int p = 0; p < FMAX / 2; ++p) {
+      x2[p] = __builtin_elementwise_fma(xp[p], sa[p], sb[p]);
+      // groups of 4 pairs: keeps the scaler reads from all being hoisted
+      // (3 x 32 transient VGPRs)
+      if ((p & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < FMAX / 2; ++p)
+      x2[p] = __builtin_elementwise_fma(f2v{xs[2 * p], xs[2 * p + 1]}, sa[p], sb[p]);
+  }
+}
+
 // ================================================================== Lloyd
 // Per-block record: [sums k*F | counts k | changed | inertia] (fp64).
 __host__ __device__ inline int lloyd_rec(int k, int F) { return k * F + k + 2; }
@@ -335,27 +499,52 @@ __host__ __device__ inline int lloyd_rec(int k, int F) { return k * F + k + 2; }
 
 // bytes of one wave's LDS region: row tile [64*FMAX] | labels [64]
 __host__ __device__ inline size_t lloyd_wave_bytes(int FMAX) { return (size_t)64 * FMAX * 4 + 64 * 4; }
+// pair-major center image (FMAX/2 x kpad4(k) float pairs)
+__host__ __device__ inline size_t cent_t_bytes(int KS, int FMAX) {
+  return (size_t)(FMAX / 2) * KS * 8;
+}
+
+// ---- wave-tile streaming with buffer loads: the resource covers a block's
+// rows from its first row to the end of the array (32-bit block-relative
+// offsets, hardware range check), the tile offset is a scalar (tile index is
+// wave-uniform) and the per-lane offsets are constants, so a tile fetch costs
+// no VALU.  Loads past the end return 0; stores past the range are dropped.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
+  const uint64_t n = nbytes < 0 ? 0 : (uint64_t)nbytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(uint32_t)(n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull),
+                                           0x00020000);
+}
+template <int NV>
+__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t rs, int soff, int lane, f4v (&v)[NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + i * 1024, soff, 0));
+}
 
 // One Lloyd pass (lloyd_iter_chunked_dense, _k_means_lloyd.pyx:23-218):
-//   mode 0: assign + relabel + per-label sums/counts (M-step partials)
-//   mode 1: assign + relabel + inertia of the new labels
-//   mode 2: inertia of the given labels (_inertia_dense, _k_means_common.pyx:94-124)
+//   MODE 0: assign + relabel + per-label sums/counts (M-step partials)
+//   MODE 1: assign + relabel + inertia of the new labels
+//   MODE 2: inertia of the given labels (_inertia_dense, _k_means_common.pyx:94-124)
 // Every wave streams its own 64-row tiles (tile w, w+nw, ... of the block's
 // row range) with the next tile's loads in flight during the current tile's
 // work; no block barrier until the final combine.
-//   E-step: lane = row, scaled row x' = x*a + b (fp32), squared distances as
-//           two interleaved fp32 FMA chains (v_pk_fma_f32), strict argmin.
+//   E-step: lane = row, scaled row x' = x*a + b (fp32), squared distances by
+//           packed-FMA chains, four centers per pass (nearest_centers), strict
+//           argmin.
 //   M-step: per-label sums of the RAW rows as a one-hot GEMM on the f32 MFMA
 //           (v_mfma_f32_16x16x4_f32: A[label][row] = onehot, B[row][feature] =
 //           x; bit-exact fp32 FMA chain in row order), 16 labels x 16 features
 //           per accumulator, flushed into fp64 registers after every 64-row
-//           tile.  The record holds a*sum(x) + b*count = sum of scaled rows.
-template <int FMAX, int MB>
-__global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X, int64_t S, int F,
+//           tile.  The LDS operands of 8 k-steps are read in one batch before
+//           their MFMAs.  The record holds a*sum(x) + b*count = sum of scaled
+//           rows.
+template <int FMAX, int MB, int MODE>
+__global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_kernel(const float* __restrict__ X, int64_t S, int F,
                                                     const float* __restrict__ ga,
                                                     const float* __restrict__ gb,
                                                     const float* __restrict__ gc, int k,
-                                                    uint8_t* __restrict__ labels, int mode,
+                                                    uint8_t* __restrict__ labels,
                                                     int64_t R, double* __restrict__ rec) {
   constexpr int NV = FMAX / 4;                   // float4 per lane per tile
   constexpr int NB = FMAX <= 16 ? 1 : FMAX / 16;  // 16-feature MFMA column blocks
@@ -363,29 +552,30 @@ __global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X,
   __shared__ __attribute__((aligned(16))) float s_a[FMAX], s_b[FMAX];
   __shared__ long long s_wcnt[4 * 64];
   __shared__ double s_red[4];
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
-  float* s_cent = reinterpret_cast<float*>(smem);  // k * FMAX (zero padded)
-  const size_t cent_bytes = ((size_t)k * FMAX * 4 + 15) & ~(size_t)15;
+  const int t = threadIdx.x, lane = t & 63, nw = blockDim.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  f2v* s_cT = reinterpret_cast<f2v*>(smem);
+  const size_t cent_bytes = cent_t_bytes(64, FMAX);
   double* s_blk = reinterpret_cast<double*>(smem + cent_bytes);  // k * F block sums
   const size_t blk_bytes = ((size_t)k * F * 8 + 15) & ~(size_t)15;
   float* s_tile = reinterpret_cast<float*>(smem + cent_bytes + blk_bytes + (size_t)wid * lloyd_wave_bytes(FMAX));
   int* s_lab = reinterpret_cast<int*>(s_tile + 64 * FMAX);
 
-  for (int q = t; q < k * FMAX; q += blockDim.x) {
-    const int j = q / FMAX, f = q - j * FMAX;
-    s_cent[q] = f < F ? gc[j * F + f] : 0.f;
-  }
+  load_centers_T<FMAX, 64>(gc, k, F, s_cT);
   for (int f = t; f < FMAX; f += blockDim.x) {
     s_a[f] = f < F ? ga[f] : 0.f;  // padded features scale to exactly 0
     s_b[f] = f < F ? gb[f] : 0.f;
   }
-  for (int q = t; q < k * F; q += blockDim.x) s_blk[q] = 0.0;
+  if (MODE == 0)
+    for (int q = t; q < k * F; q += blockDim.x) s_blk[q] = 0.0;
   __syncthreads();
 
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
   const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
   const int64_t total = S * (int64_t)F, n4 = total >> 2;
-  const f4v* X4 = reinterpret_cast<const f4v*>(X);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + lo * F, (S - lo) * F * 4);
+  const __amdgpu_buffer_rsrc_t rl = make_rsrc(labels + lo, hi - lo);
+  const int tile_bytes = 64 * F * 4;
   const int kk = lane >> 4, jj = lane & 15;  // MFMA operand lane map
   double inert = 0.0;
   long long changed = 0, cnt = 0;
@@ -402,15 +592,8 @@ __global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X,
   // fetch tile `tt` (clamped to the last tile: a harmless re-read)
   auto fetch = [&](int tt) {
     tt = tt < ntile ? tt : ntile - 1;
-    const int64_t r = lo + (int64_t)tt * 64;
-    old_next = labels[min(r + lane, hi - 1)];
-    const int64_t q0 = (r * F) >> 2;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      int64_t q = q0 + lane + i * 64;
-      q = q < n4 ? q : n4 - 1;
-      v[i] = X4[q];
-    }
+    old_next = __builtin_amdgcn_raw_buffer_load_b8(rl, lane, tt * 64, 0);
+    tile_load<NV>(rx, tt * tile_bytes, lane, v);
   };
   int tc = wid;
   if (tc < ntile) fetch(tc);
@@ -428,51 +611,30 @@ __global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X,
     const bool valid = lane < nrow;
     // ---- E-step ----
     f2v x2[FMAX / 2];
-    {
-      const float* xs = s_tile + lane * F;
-      // re-read the scaler from LDS every tile instead of pinning 2*FMAX
-      // loop-invariant registers (they would spill)
-      int z = 0;
-      asm volatile("" : "+s"(z));
-      const f2v* sa = reinterpret_cast<const f2v*>(s_a) + z;
-      const f2v* sb = reinterpret_cast<const f2v*>(s_b) + z;
-#pragma unroll
-      for (int p = 0; p < FMAX / 2; ++p)
-        x2[p] = __builtin_elementwise_fma(f2v{xs[2 * p], xs[2 * p + 1]}, sa[p], sb[p]);
-    }
+    load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
     int lab;
     float best;
-    if (mode == 2) {
+    if (MODE == 2) {
       lab = old;
-      const f2v* c2 = reinterpret_cast<const f2v*>(s_cent + lab * FMAX);
       f2v acc = f2v{0.f, 0.f};
 #pragma unroll
       for (int p = 0; p < FMAX / 2; ++p) {
-        const f2v d = x2[p] - c2[p];
+        const f2v d = x2[p] - s_cT[p * 64 + lab];
         acc = __builtin_elementwise_fma(d, d, acc);
       }
       best = acc.x + acc.y;
     } else {
-      lab = 0;
-      best = 0.f;
-      for (int j = 0; j < k; ++j) {
-        const f2v* c2 = reinterpret_cast<const f2v*>(s_cent + j * FMAX);
-        f2v acc = f2v{0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < FMAX / 2; ++p) {
-          const f2v d = x2[p] - c2[p];
-          acc = __builtin_elementwise_fma(d, d, acc);
-        }
-        const float dd = acc.x + acc.y;
-        if (j == 0 || dd < best) { best = dd; lab = j; }
-      }
-      if (valid) {
-        changed += (lab != old) ? 1 : 0;
-        labels[r0 + lane] = (uint8_t)lab;
-      }
+      float m2u;
+#ifdef MW_X_NOE
+      lab = old; best = x2[0].x;
+#else
+      nearest_centers<FMAX, 64, false>(x2, s_cT, k, lab, best, m2u);
+#endif
+      changed += (valid && lab != old) ? 1 : 0;
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)lab, rl, lane, tc * 64, 0);
     }
-    if (mode >= 1 && valid) inert += (double)best;
-    if (mode == 0) {
+    if (MODE >= 1 && valid) inert += (double)best;
+    if (MODE == 0) {
       // ---- M-step partials ----
       s_lab[lane] = valid ? lab : -1;
       for (int j = 0; j < k; ++j) {
@@ -484,22 +646,30 @@ __global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X,
       for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) d[mb][nb] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int st = 0; st < 16; ++st) {  // 4 rows per MFMA k-step
-        const int r = 4 * st + kk;
-        const int L = s_lab[r];
-        float b[NB];
+      const float* xrow = s_tile + kk * F;  // row 4*st + kk at + 4*st*F
+      int bcol[NB];
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          const int f = 16 * nb + jj;  // columns past F are never read back
-          b[nb] = s_tile[r * F + (f < F ? f : F - 1)];
+      for (int nb = 0; nb < NB; ++nb) bcol[nb] = min(16 * nb + jj, F - 1);  // cols >= F never read back
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // two batches of 8 k-steps (4 rows each)
+        int Lr[8];
+        float xb[8][NB];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int st = 8 * h + u;
+          Lr[u] = s_lab[4 * st + kk];
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) xb[u][nb] = xrow[4 * st * F + bcol[nb]];
         }
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-          const float a = (L == 16 * mb + jj) ? 1.f : 0.f;
+        for (int u = 0; u < 8; ++u) {
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb)
-            d[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[nb], d[mb][nb], 0, 0, 0);
+          for (int mb = 0; mb < MB; ++mb) {
+            const float a = (Lr[u] == 16 * mb + jj) ? 1.f : 0.f;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+              d[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xb[u][nb], d[mb][nb], 0, 0, 0);
+          }
         }
       }
 #pragma unroll
@@ -514,9 +684,9 @@ __global__ void __launch_bounds__(256) lloyd_kernel(const float* __restrict__ X,
   s_wcnt[wid * 64 + lane] = cnt;
   const double ch = block_sum((double)changed, s_red);
   const double in = block_sum(inert, s_red);
-  const int rl = lloyd_rec(k, F);
-  double* out = rec + (size_t)blockIdx.x * rl;
-  if (mode == 0) {
+  const int rlen = lloyd_rec(k, F);
+  double* out = rec + (size_t)blockIdx.x * rlen;
+  if (MODE == 0) {
     for (int w = 0; w < nw; ++w) {
       if (wid == w) {
 #pragma unroll
@@ -651,8 +821,8 @@ __host__ __device__ inline size_t assign_wave_bytes(int k, int CMAX) {
 // (d2 - d1) / d2 from the two smallest distances, -1 / NaN outside the mask.
 // Per-block record: [sum conf k | count k] (fp64, fixed combine order).
 // Waves stream 64-pixel tiles (64*C floats) with the next tile in flight.
-template <int CMAX>
-__global__ void __launch_bounds__(256) assign_kernel(const float* __restrict__ img, int C,
+template <int CMAX, int KS>
+__global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float* __restrict__ img, int C,
                                                      const int32_t* __restrict__ feat, int F,
                                                      const float* __restrict__ ga,
                                                      const float* __restrict__ gb,
@@ -666,22 +836,23 @@ __global__ void __launch_bounds__(256) assign_kernel(const float* __restrict__ i
   __shared__ __attribute__((aligned(16))) float s_a[CMAX], s_b[CMAX];
   __shared__ int s_feat[CMAX];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
-  float* s_cent = reinterpret_cast<float*>(smem);  // k * CMAX (zero padded)
-  const size_t cent_bytes = ((size_t)k * CMAX * 4 + 15) & ~(size_t)15;
+  f2v* s_cT = reinterpret_cast<f2v*>(smem);  // pair-major centers
+  const size_t cent_bytes = cent_t_bytes(KS, CMAX);
+  __shared__ int s_ident;
   // per wave: conf sums fp64 [k+1][64] | counts u32 [k+1][64] | tile [64*CMAX]
   const size_t wslot = assign_wave_bytes(k, CMAX);
   char* wb = smem + cent_bytes + (size_t)wid * wslot;
   double* w_csum = reinterpret_cast<double*>(wb);
   unsigned* w_ccnt = reinterpret_cast<unsigned*>(w_csum + (k + 1) * 64);
   float* s_tile = reinterpret_cast<float*>(w_ccnt + (k + 1) * 64);
-  for (int q = t; q < k * CMAX; q += blockDim.x) {
-    const int j = q / CMAX, f = q - j * CMAX;
-    s_cent[q] = f < F ? gc[j * F + f] : 0.f;
-  }
+  load_centers_T<CMAX, KS>(gc, k, F, s_cT);
+  if (t == 0) s_ident = F == C;
+  __syncthreads();
   for (int f = t; f < CMAX; f += blockDim.x) {
     s_feat[f] = f < F ? feat[f] : 0;
     s_a[f] = f < F ? ga[f] : 0.f;
     s_b[f] = f < F ? gb[f] : 0.f;
+    if (f < F && feat[f] != f) s_ident = 0;  // features = all channels in order
   }
   for (int q = lane; q < (k + 1) * 64; q += 64) {
     w_csum[q] = 0.0;
@@ -693,6 +864,7 @@ __global__ void __launch_bounds__(256) assign_kernel(const float* __restrict__ i
   const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
   const int64_t total = n * (int64_t)C, n4 = total >> 2;
   const f4v* X4 = reinterpret_cast<const f4v*>(img);
+  const bool ident = s_ident != 0;
 
   f4v v[NV];
   int mask_next = 0;
@@ -721,31 +893,23 @@ __global__ void __launch_bounds__(256) assign_kernel(const float* __restrict__ i
     wt_tail(np * C, p0 * C, n4, img, total, s_tile, lane);
     const int mk = mask_next;
     fetch(tc + nw);
-    int z = 0;
-    asm volatile("" : "+s"(z));
-    const f2v* sa = reinterpret_cast<const f2v*>(s_a) + z;
-    const f2v* sb = reinterpret_cast<const f2v*>(s_b) + z;
-    const int* sf = s_feat + z;
-    const float* xs = s_tile + lane * C;
     f2v x2[CMAX / 2];
+    if (ident) {
+      load_scaled_row<CMAX>(s_tile, lane, C, s_a, s_b, x2);
+    } else {
+      int z = 0;
+      asm volatile("" : "+s"(z));
+      const f2v* sa = reinterpret_cast<const f2v*>(s_a) + z;
+      const f2v* sb = reinterpret_cast<const f2v*>(s_b) + z;
+      const int* sf = s_feat + z;
+      const float* xs = s_tile + lane * C;
 #pragma unroll
-    for (int p = 0; p < CMAX / 2; ++p)
-      x2[p] = __builtin_elementwise_fma(f2v{xs[sf[2 * p]], xs[sf[2 * p + 1]]}, sa[p], sb[p]);
-    float m1 = 0.f, m2 = __builtin_inff();
-    int lab = 0;
-    for (int j = 0; j < k; ++j) {
-      const f2v* c2 = reinterpret_cast<const f2v*>(s_cent + j * CMAX);
-      f2v acc = f2v{0.f, 0.f};
-#pragma unroll
-      for (int p = 0; p < CMAX / 2; ++p) {
-        const f2v d = x2[p] - c2[p];
-        acc = __builtin_elementwise_fma(d, d, acc);
-      }
-      const float dd = acc.x + acc.y;
-      if (j == 0) { m1 = dd; lab = 0; }
-      else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
-      else if (dd < m2) { m2 = dd; }
+      for (int p = 0; p < CMAX / 2; ++p)
+        x2[p] = __builtin_elementwise_fma(f2v{xs[sf[2 * p]], xs[sf[2 * p + 1]]}, sa[p], sb[p]);
     }
+    float m1, m2;
+    int lab;
+    nearest_centers<CMAX, KS, true>(x2, s_cT, k, lab, m1, m2);
     const bool valid = lane < np;
     const bool in_mask = valid && mk != 0;
     const float conf = in_mask ? (m2 - m1) / m2 : __builtin_nanf("");
@@ -930,22 +1094,27 @@ int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a, const fl
   double* rec = reinterpret_cast<double*>(d_ws);
   const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
   const int MBv = k <= 16 ? 1 : k <= 32 ? 2 : 4;
-  const size_t cent = ((size_t)k * FM * 4 + 15) & ~(size_t)15;
+  const size_t cent = cent_t_bytes(64, FM);
   const size_t blk = ((size_t)k * F * 8 + 15) & ~(size_t)15;
   const size_t lds = cent + blk + 4 * lloyd_wave_bytes(FM);
-#define MW_LL(FMV, MBV)                                                                        \
-  hipLaunchKernelGGL((lloyd_kernel<FMV, MBV>), dim3(G), dim3(256), lds, s, d_X, S, F, d_a,    \
-                     d_b, d_centers, k, d_labels, mode, R, rec)
+#define MW_LLM(FMV, MBV, MO)                                                                   \
+  hipLaunchKernelGGL((lloyd_kernel<FMV, MBV, MO>), dim3(G), dim3(256), lds, s, d_X, S, F, d_a, \
+                     d_b, d_centers, k, d_labels, R, rec)
+#define MW_LL(FMV, MBV)              \
+  if (mode == 0) MW_LLM(FMV, MBV, 0); \
+  else if (mode == 1) MW_LLM(FMV, 1, 1); \
+  else MW_LLM(FMV, 1, 2);
 #define MW_LLF(FMV)                \
-  if (MBv == 1) MW_LL(FMV, 1);     \
-  else if (MBv == 2) MW_LL(FMV, 2); \
-  else MW_LL(FMV, 4);
+  if (MBv == 1) { MW_LL(FMV, 1) }     \
+  else if (MBv == 2) { MW_LL(FMV, 2) } \
+  else { MW_LL(FMV, 4) }
   if (FM == 8) { MW_LLF(8) }
   else if (FM == 16) { MW_LLF(16) }
   else if (FM == 32) { MW_LLF(32) }
   else { MW_LLF(64) }
 #undef MW_LLF
 #undef MW_LL
+#undef MW_LLM
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
@@ -1005,9 +1174,9 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
   const int G = kblocks(n_pix);
   const int64_t R = krows(n_pix);
   double* rec = reinterpret_cast<double*>(d_ws);
-#define MW_AS(CM)                                                                               \
+#define MW_AS(CM, KSV)                                                                          \
   {                                                                                             \
-    const size_t cent = ((size_t)k * CM * 4 + 15) & ~(size_t)15;                                \
+    const size_t cent = cent_t_bytes(KSV, CM);                                                  \
     int nw = 4;                                                                                 \
     while (nw > 1 && cent + nw * assign_wave_bytes(k, CM) > 160 * 1024) --nw;                   \
     const size_t lds = cent + nw * assign_wave_bytes(k, CM);                                    \
@@ -1015,13 +1184,17 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
       set_error("mw_assign_conf: LDS %zu too large (C=%d k=%d)", lds, C, k);                    \
       return MW_EUNSUPPORTED;                                                                   \
     }                                                                                           \
-    hipLaunchKernelGGL(assign_kernel<CM>, dim3(G), dim3(64 * nw), lds, s, d_img, C, d_feat, F,  \
-                       d_a, d_b, d_centers, k, d_mask, n_pix, R, d_label, d_conf, rec);         \
+    hipLaunchKernelGGL((assign_kernel<CM, KSV>), dim3(G), dim3(64 * nw), lds, s, d_img, C,      \
+                       d_feat, F, d_a, d_b, d_centers, k, d_mask, n_pix, R, d_label, d_conf, rec); \
   }
-  if (C <= 8) MW_AS(8)
-  else if (C <= 16) MW_AS(16)
-  else if (C <= 32) MW_AS(32)
-  else MW_AS(64)
+#define MW_ASK(CM)             \
+  if (k <= 64) MW_AS(CM, 64)   \
+  else MW_AS(CM, 128)
+  if (C <= 8) { MW_ASK(8) }
+  else if (C <= 16) { MW_ASK(16) }
+  else if (C <= 32) { MW_ASK(32) }
+  else { MW_ASK(64) }
+#undef MW_ASK
 #undef MW_AS
   MW_LAUNCH_CHECK();
   return MW_OK;
