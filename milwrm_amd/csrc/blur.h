@@ -33,6 +33,12 @@ constexpr int kBlurMaxL = 2;     // input-row pair loads per thread per row (BW 
 
 typedef float bf2 __attribute__((ext_vector_type(2)));
 
+// fused fast paths (matrix-core kernel, then the VALU kernel below), defined in
+// blur_mfma.h and instantiated per dtype in blur_{u8,u16,f32}.hip
+template <typename T>
+int launch_blur_fast(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                     const struct BlurTaps& taps, int r, float* out, hipStream_t st);
+
 // accurate log10(t + p) for t >= 0 (log1p-style correction of the rounding
 // of t + p, so small t keep full relative accuracy)
 __device__ __forceinline__ float lognorm1(float x, float inv, float p) {
@@ -293,7 +299,7 @@ static int launch_blur_r(const T* in, int H, int W, int C, const float* inv_mean
 // Fast path for even C <= 64 and r <= kBlurMaxR; MW_EUNSUPPORTED otherwise
 // (the caller then takes the two-pass fallback).
 template <typename T>
-int launch_blur_fast(const T* in, int H, int W, int C, const float* inv_mean, float p,
+int launch_blur_valu(const T* in, int H, int W, int C, const float* inv_mean, float p,
                      const BlurTaps& taps, int r, float* out, hipStream_t st) {
   if (C % 2 != 0 || C > 64 || r < 0 || r > kBlurMaxR) return MW_EUNSUPPORTED;
   switch (r) {

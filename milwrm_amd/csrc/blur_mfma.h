@@ -1,0 +1,420 @@
+// Fused log-normalise + separable Gaussian blur with the horizontal pass on
+// the f32 matrix cores (img.log_normalize + img.blurring('gaussian'),
+// MxIF.py:416-455 / 375-394; scipy gaussian_filter mode='nearest', truncate=4)
+// — the fast path for radius 1..8 (sigma <= 2.1) and even C <= 64.
+//
+// A workgroup owns a band of BW = 16*BT output columns x kBlurBH output rows
+// and all channels; wave (tx, ct) owns the 16-column x 16-channel output tile
+// (BT x ceil(C/16) waves).  Rows stream top to bottom through three stages:
+//   1. input: the halo'd row segment (BW + 2r columns x C channels, one
+//      contiguous HWC byte range) arrives as 16-byte buffer loads issued a few
+//      rows ahead (register ring), is log-normalised and stored as fp32 to a
+//      double-buffered LDS row [column][16 * ceil(C/16) channels] (channel
+//      tiles XOR-swizzled by column parity when the pitch is a multiple of 32
+//      floats: conflict-free operand reads; pad channels stay 0; at the slide
+//      edges the clamped halo columns are copied from the edge column);
+//   2. horizontal pass = one GEMM per tile: out[16 cols][16 ch] = T[16][4K] x
+//      in[4K cols][16 ch], T the banded Toeplitz matrix of the 2r+1 taps
+//      (constant A operands), K/4 v_mfma_f32_16x16x4_f32 in two interleaved
+//      accumulators.  The f32 MFMA is an exact fp32 FMA chain, and the zero
+//      band entries add exact zeros;
+//   3. vertical pass: the last 2r+1 horizontal results (4 columns x 1 channel
+//      per lane: the MFMA D layout) sit in a register ring (static indices:
+//      the row loop is unrolled by 2r+1) and are combined by packed FMAs into
+//      an LDS staging row laid out like the output (HWC), which the whole
+//      workgroup writes to HBM as 16-byte stores one step later.
+// Every HBM access is 16 bytes per lane (a blur-shaped access probe on the
+// MI355X, tools/probe/band_probe.hip: 4-byte lanes 4.0 TB/s, 16-byte lanes
+// 5.2 TB/s); the matrix pipe takes the horizontal taps, the VALU the vertical
+// ones and the log-normalise; one workgroup barrier per row.
+#pragma once
+
+#include "blur.h"
+
+namespace mw {
+
+constexpr int kBlurMfmaMaxR = 8;
+
+typedef float f4m __attribute__((ext_vector_type(4)));
+typedef unsigned int u4m __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t blur_rsrc(const void* base, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
+}
+
+// element pair i (0-based) of a 16-byte chunk as floats
+template <typename T> struct Chunk16;
+template <> struct Chunk16<uint8_t> {
+  static constexpr int P = 8;
+  static __device__ __forceinline__ bf2 pair(const u4m& v, int i) {
+    const uint32_t w = v[i >> 1] >> (16 * (i & 1));
+    return bf2{(float)(w & 0xffu), (float)((w >> 8) & 0xffu)};
+  }
+};
+template <> struct Chunk16<uint16_t> {
+  static constexpr int P = 4;
+  static __device__ __forceinline__ bf2 pair(const u4m& v, int i) {
+    return bf2{(float)(v[i] & 0xffffu), (float)(v[i] >> 16)};
+  }
+};
+template <> struct Chunk16<float> {
+  static constexpr int P = 2;
+  static __device__ __forceinline__ bf2 pair(const u4m& v, int i) {
+    return bf2{__builtin_bit_cast(float, v[2 * i]), __builtin_bit_cast(float, v[2 * i + 1])};
+  }
+};
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a
+// workgroup-scope acq_rel fence + s_barrier, and hipcc lowers the fence to
+// s_waitcnt vmcnt(0) whenever a global store is outstanding — which also
+// drains the input loads in flight (one counter) and flattens the row
+// pipeline.  Nothing here hands data between threads through global memory.
+__device__ __forceinline__ uint32_t lds_addr_u32(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// LDS-DMA of 16 bytes per lane: global (SGPR base + per-lane 32-bit offset)
+// -> LDS at (wave-uniform lds_dst) + lane * 16, no VGPR destination.  Inline
+// asm (recipe: cdna_hip_programming.md §5.4), so hipcc neither counts it nor
+// drains it: the kernel waits for it with counted vmcnt before the barrier
+// that precedes the read.  The offset VGPR is set once per thread and never
+// rewritten, so no later instruction can race the DMA's operand read; the
+// string opens with s_nop 4 (SGPR base fresh from VALU/readfirstlane).
+__device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_dst)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <typename T, int R, int CT, int BT>
+struct BlurMfmaCfg {
+  static constexpr int NR = 2 * R + 1;
+  static constexpr int BW = 16 * BT;            // output columns per band
+  static constexpr int NPX = BW + 2 * R;        // halo'd input columns
+  static constexpr int PS = 16 * CT;            // LDS row pitch per column (floats)
+  static constexpr bool SWZ = (PS % 32) == 0;   // swizzle channel tiles by column parity
+  static constexpr int NK = (16 + 2 * R + 3) / 4;  // MFMA k-steps (4 input columns each)
+  static constexpr int NT = 64 * BT * CT;
+  static constexpr int NW = NT / 64;
+  static constexpr int ROW = NPX * PS;          // floats per LDS fp32 row buffer
+  static constexpr int STG = BW * 16 * CT;      // floats per LDS output staging row (>= BW*C)
+  // raw input row segment: <= NPX * C elements, C <= 16*CT; NG 1-KB DMA pieces per wave
+  static constexpr int SEGMAX = NPX * 16 * CT * (int)sizeof(T);
+  static constexpr int NG = (SEGMAX + NW * 1024 - 1) / (NW * 1024);
+  static constexpr int SLOT = NG * NW * 1024;   // bytes per raw ring slot
+  static constexpr int NCH = SLOT / 16 / NT;    // 16-byte chunks per thread (= NG)
+  static constexpr int NP = NCH * Chunk16<T>::P;  // element pairs per thread
+  static constexpr size_t FIXED = (2 * (size_t)ROW + 2 * (size_t)STG) * sizeof(float) + 64;
+  // raw ring depth: 5 rows (4 in flight) when two workgroups then fit a CU's
+  // 160 KB of LDS, else as deep as one workgroup allows (<= 9); >= 4 (the
+  // launcher rejects configurations whose LDS does not fit)
+  static constexpr int D2 = ((80 * 1024 - (int)FIXED) / SLOT);
+  static constexpr int D1 = ((160 * 1024 - (int)FIXED) / SLOT);
+#ifdef MW_BLUR_D
+  static constexpr int D = D1 >= MW_BLUR_D ? MW_BLUR_D : 4;
+#else
+  static constexpr int D = D2 >= 5 ? 5 : (D1 >= 9 ? 9 : (D1 >= 4 ? D1 : 4));
+#endif
+  static constexpr int LA = D - 1;              // rows in flight ahead of the converted one
+  static constexpr size_t lds_bytes() { return FIXED + (size_t)D * SLOT; }
+};
+
+template <typename T, int R, int CT, int BT, bool LOGN>
+__global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __restrict__ in, int H, int W,
+                                                                 int C, const float* __restrict__ inv_mean,
+                                                                 float pseudo, BlurTaps taps,
+                                                                 float* __restrict__ out) {
+  using K = BlurMfmaCfg<T, R, CT, BT>;
+  constexpr int NR = K::NR, BW = K::BW, NPX = K::NPX, PS = K::PS, NK = K::NK, NT = K::NT;
+  constexpr int ROW = K::ROW, STG = K::STG, NCH = K::NCH, NP = K::NP, CP = Chunk16<T>::P;
+  constexpr int NG = K::NG, SLOT = K::SLOT, D = K::D, LA = K::LA;
+  constexpr bool SWZ = K::SWZ;
+  static_assert(LA >= 3, "raw ring too shallow");
+  // one step issues NG DMA pieces + 1 output store per wave; the DMA of row
+  // s+2 (issued at step s+2-LA) is followed by LA-2 steps' worth of them
+  constexpr int kWaitSteady = (LA - 2) * (NG + 1);
+  constexpr int kWaitEarly = (LA - 2) * NG + 1;  // steps s < LA-2 (prologue DMAs, no stores)
+  static_assert(kWaitSteady <= 63, "vmcnt field is 6 bits");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* s_rows = smem;                       // 2 x ROW  (fp32 input rows)
+  float* s_stg = smem + 2 * ROW;              // 2 x STG  (output staging rows, HWC)
+  float* s_dummy = smem + 2 * ROW + 2 * STG;  // 64 bytes: sink of pad pairs
+  char* s_raw = reinterpret_cast<char*>(smem) + K::FIXED;  // D x SLOT raw input rows
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int tx = wv % BT, ct = wv / BT;
+  const int x0 = blockIdx.x * BW;
+  const int y0 = blockIdx.y * kBlurBH;
+  const int y1 = min(H, y0 + kBlurBH);
+  const int nrows = (y1 - y0) + 2 * R;
+  const int bw = min(BW, W - x0);
+  // clamped input column range [xa, xb) and its position in the halo'd row
+  const int xa = max(0, x0 - R), xb = min(W, x0 + BW + R);
+  const int col_a = xa - (x0 - R);
+  const bool edge = (xa != x0 - R) || (xb != x0 + BW + R);
+  const uint32_t seg_bytes = (uint32_t)(xb - xa) * (uint32_t)C * sizeof(T);
+
+  for (int q = t; q < 2 * ROW; q += NT) s_rows[q] = 0.f;  // pad channels stay 0
+
+  // ---- raw chunks of this thread (chunk t + c*NT of a slot): LDS fp32
+  // destination of each element pair in a row buffer (-1: pad pair, written
+  // to the sink)
+  int p_dst[NP];
+  bf2 p_inv[NP];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const uint32_t b0 = (uint32_t)(t + c * NT) * 16u;
+#pragma unroll
+    for (int i = 0; i < CP; ++i) {
+      const uint32_t e = (b0 / (uint32_t)sizeof(T)) + 2u * i;  // element index in the segment
+      const bool ok = e * (uint32_t)sizeof(T) < seg_bytes;
+      const int px = ok ? (int)(e / (uint32_t)C) : 0;
+      const int ch = ok ? (int)(e - (uint32_t)px * C) : 0;
+      const int col = col_a + px, ctile = ch >> 4;
+      p_dst[c * CP + i] = ok ? col * PS + 16 * (SWZ ? (ctile ^ (col & 1)) : ctile) + (ch & 15) : -1;
+      p_inv[c * CP + i] = (LOGN && ok) ? bf2{inv_mean[ch], inv_mean[ch + 1]} : bf2{1.f, 1.f};
+    }
+  }
+  // DMA source offset of this lane's piece g: chunk t + g*NT, clamped into the segment
+  uint32_t g_off[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const uint32_t b = (uint32_t)(t + g * NT) * 16u;
+    g_off[g] = b < seg_bytes ? b : 0u;
+  }
+  const uint32_t raw0 = lds_addr_u32(s_raw);
+
+  // ---- MFMA operands: A = banded Toeplitz taps (row m = output column, k =
+  // input column of the tile's halo'd span), B = LDS row reads
+  const int m = lane & 15, kq = lane >> 4;
+  float a_op[NK];
+#pragma unroll
+  for (int st = 0; st < NK; ++st) {
+    const int j = 4 * st + kq - m;
+    a_op[st] = (j >= 0 && j <= 2 * R) ? taps.w[j] : 0.f;
+  }
+  // B[k][n] for k-step st: column 16*tx + 4*st + kq, channel 16*ct + n (n = m)
+  const int b_ct = SWZ ? (ct ^ (kq & 1)) : ct;  // (16*tx + 4*st + kq) & 1 == kq & 1
+  const int b_base = (16 * tx + kq) * PS + 16 * b_ct + m;
+  // staging slot of D[r]: column 16*tx + 4*kq + r, channel 16*ct + m (HWC, pitch C)
+  const bool st_ok = 16 * ct + m < C;
+  const int st_base = (16 * tx + 4 * kq) * C + 16 * ct + m;
+  // output: the band's row segment is bw*C floats (a multiple of 4: host
+  // check); thread t stores 16-byte chunk t, past the segment the range check drops it
+  const uint32_t out_bytes = (uint32_t)bw * (uint32_t)C * 4u;
+
+  f4m ring[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) ring[j] = f4m{0.f, 0.f, 0.f, 0.f};
+
+  // DMA of input row q (clamped; past the band: a harmless re-read) into slot q % D
+  auto dma_row = [&](int q) {
+    int yy = y0 - R + q;
+    yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
+    const char* src = reinterpret_cast<const char*>(in + ((int64_t)yy * W + xa) * C);
+    const uint32_t slot = raw0 + (uint32_t)(q % D) * SLOT;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) glds16(src, g_off[g], slot + (uint32_t)(g * NT + 64 * wv) * 16u);
+  };
+  auto convert_row = [&](int q) {
+    float* dst = s_rows + (q & 1) * ROW;
+    const char* raw = s_raw + (q % D) * SLOT;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const u4m v = *reinterpret_cast<const u4m*>(raw + (t + c * NT) * 16);
+#pragma unroll
+      for (int i = 0; i < CP; ++i) {
+        bf2 x = Chunk16<T>::pair(v, i);
+#ifndef MW_X_NOLOG
+        if (LOGN) x = lognorm2(x, p_inv[c * CP + i], pseudo);
+#endif
+        const int d = p_dst[c * CP + i];
+        *reinterpret_cast<bf2*>(d >= 0 ? dst + d : s_dummy) = x;  // pad pairs: the sink
+      }
+    }
+    if (edge) {  // clamped halo columns ('nearest'): copies of the edge column
+      lds_barrier();
+      const int nl = col_a, nr = NPX - (col_a + (xb - xa));
+      for (int q2 = t; q2 < (nl + nr) * PS; q2 += NT) {
+        const int h = q2 / PS, f = q2 - h * PS;
+        const int col = h < nl ? h : col_a + (xb - xa) + (h - nl);
+        const int src = h < nl ? col_a : col_a + (xb - xa) - 1;
+        // (the channel-tile swizzle depends on the column parity)
+        const int ctile = f >> 4;
+        const int fs = SWZ ? 16 * (ctile ^ (src & 1)) + (f & 15) : f;
+        const int fd = SWZ ? 16 * (ctile ^ (col & 1)) + (f & 15) : f;
+        dst[col * PS + fd] = dst[src * PS + fs];
+      }
+    }
+  };
+  // one 16-byte store per thread and step; rows outside the band are dropped
+  // by an empty range (every step issues exactly one store: counted waits)
+  auto store_out = [&](int stg_buf, int yo, bool valid) {
+    const f4m v = *reinterpret_cast<const f4m*>(s_stg + stg_buf * STG + 4 * t);
+    const __amdgpu_buffer_rsrc_t ro =
+        blur_rsrc(out + ((int64_t)(valid ? yo : 0) * W + x0) * C, valid ? out_bytes : 0u);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4m, v), ro, t * 16, 0, 0);
+  };
+
+  lds_barrier();  // zero fill done
+#pragma unroll
+  for (int q = 0; q < LA; ++q) dma_row(q);
+  vm_wait_n<(LA - 1) * NG>();  // row 0 landed (this wave's pieces)
+  lds_barrier();
+  convert_row(0);
+  vm_wait_n<(LA - 2) * NG>();  // row 1 landed
+  lds_barrier();
+  // step s: convert input row s+1, MFMA row s, vertical pass of row s-1 into
+  // staging, store the output row staged at step s-1, DMA of row s+LA; wait
+  // for row s+2's DMA; one barrier
+  const int nsteps = nrows + 2;
+  // One row step (j = s mod NR is a compile-time constant after unrolling, so
+  // the ring indices are static).  GUARD false: the steady state, where every
+  // stage is live, with no branches, so hipcc can interleave the stages.
+  auto step = [&](const int s, const int j, const bool guard) {
+    if (!guard || s + 1 < nrows) convert_row(s + 1);
+    float b_op[NK];
+    if (!guard || s < nrows) {
+      const float* rowp = s_rows + (s & 1) * ROW + b_base;
+#pragma unroll
+      for (int st = 0; st < NK; ++st) b_op[st] = rowp[4 * st * PS];
+    }
+    if (!guard || (s >= 1 && s - 1 >= 2 * R && s - 1 < nrows)) {
+      // vertical pass of row s-1 over ring rows s-1-2R .. s-1 (slots j .. j+2R)
+      bf2 v0 = bf2{0.f, 0.f}, v1 = bf2{0.f, 0.f}, u0 = bf2{0.f, 0.f}, u1 = bf2{0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const f4m& rg = ring[(j + i) % NR];
+        const bf2 w2 = bf2{taps.w[i], taps.w[i]};
+        if (i & 1) {
+          v1 = __builtin_elementwise_fma(w2, bf2{rg.x, rg.y}, v1);
+          u1 = __builtin_elementwise_fma(w2, bf2{rg.z, rg.w}, u1);
+        } else {
+          v0 = __builtin_elementwise_fma(w2, bf2{rg.x, rg.y}, v0);
+          u0 = __builtin_elementwise_fma(w2, bf2{rg.z, rg.w}, u0);
+        }
+      }
+      const bf2 va = v0 + v1, vb = u0 + u1;
+      if (st_ok) {
+        float* sg = s_stg + ((s - 1) & 1) * STG + st_base;
+        sg[0] = va.x;
+        sg[C] = va.y;
+        sg[2 * C] = vb.x;
+        sg[3 * C] = vb.y;
+      }
+    }
+    store_out(s & 1, y0 + s - 2 - 2 * R, !guard || s >= 2 + 2 * R);
+    dma_row(s + LA);
+    if (!guard || s < nrows) {
+      f4m d0 = f4m{0.f, 0.f, 0.f, 0.f}, d1 = f4m{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < NK; st += 2) {
+        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a_op[st], b_op[st], d0, 0, 0, 0);
+        if (st + 1 < NK) d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a_op[st + 1], b_op[st + 1], d1, 0, 0, 0);
+      }
+      ring[j] = d0 + d1;
+    }
+    if (guard && s < LA - 2) vm_wait_n<kWaitEarly>();
+    else vm_wait_n<kWaitSteady>();
+    lds_barrier();
+  };
+  // steady groups: NR-aligned, all of s in [2R+2, nrows-2], interior bands
+  // (edge bands copy halo columns behind an extra barrier: guarded path)
+  const int g0 = 2 * NR;  // first multiple of NR >= 2R+2
+  const int g1 = edge ? g0 : max(g0, ((nrows - 1) / NR) * NR);  // groups [g0, g1) are steady
+  int base = 0;
+  for (; base < g0 && base < nsteps; base += NR) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      if (base + j < nsteps) step(base + j, j, true);
+  }
+  for (; base < g1; base += NR) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j) step(base + j, j, false);
+  }
+  for (; base < nsteps; base += NR) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      if (base + j < nsteps) step(base + j, j, true);
+  }
+  vm_wait_n<0>();  // no DMA may still target this workgroup's LDS at exit
+}
+
+template <typename T, int R, int CT, int BT>
+static int launch_blur_mfma_rc(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                               const BlurTaps& taps, float* out, hipStream_t st) {
+  using K = BlurMfmaCfg<T, R, CT, BT>;
+  const size_t lds = K::lds_bytes();
+  if (lds > 160 * 1024 || K::D < 4) return MW_EUNSUPPORTED;
+  dim3 grid((W + K::BW - 1) / K::BW, (H + kBlurBH - 1) / kBlurBH);
+  if (inv_mean)
+    hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, true>), grid, dim3(K::NT), lds, st, in, H, W,
+                       C, inv_mean, p, taps, out);
+  else
+    hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, false>), grid, dim3(K::NT), lds, st, in, H, W,
+                       C, inv_mean, p, taps, out);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+template <typename T, int R>
+static int launch_blur_mfma_r(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                              const BlurTaps& taps, float* out, hipStream_t st) {
+  static const int bt = [] {  // column tiles per band (tuning override MW_BLUR_BT = 2 or 4)
+    const char* e = getenv("MW_BLUR_BT");
+    return (e && atoi(e) == 2) ? 2 : 4;
+  }();
+#define MW_BT(CTV)                                                                            \
+  return bt == 4 ? launch_blur_mfma_rc<T, R, CTV, 4>(in, H, W, C, inv_mean, p, taps, out, st) \
+                 : launch_blur_mfma_rc<T, R, CTV, 2>(in, H, W, C, inv_mean, p, taps, out, st);
+  if (C <= 16) { MW_BT(1) }
+  if (C <= 32) { MW_BT(2) }
+  if (C <= 48) { MW_BT(3) }
+  MW_BT(4)
+#undef MW_BT
+}
+
+// MFMA path for even C <= 64, 1 <= r <= 8, rows that fit 32-bit offsets;
+// MW_EUNSUPPORTED otherwise (the caller tries the next path).
+template <typename T>
+int launch_blur_mfma(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                     const BlurTaps& taps, int r, float* out, hipStream_t st) {
+  if (C % 2 != 0 || C > 64 || r < 1 || r > kBlurMfmaMaxR) return MW_EUNSUPPORTED;
+  // 16-byte output chunks: every band's row segment is a whole number of them
+  if (((int64_t)W * C) % 4 != 0) return MW_EUNSUPPORTED;
+  // 16-byte DMA pieces read whole dwords of the input rows
+  if (((int64_t)W * C * (int64_t)sizeof(T)) % 4 != 0) return MW_EUNSUPPORTED;
+  if ((int64_t)W * C * 4 >= 0x7FFFFFF0ll) return MW_EUNSUPPORTED;
+  if (const char* e = getenv("MW_BLUR_IMPL"))
+    if (e[0] == 'v') return MW_EUNSUPPORTED;  // force the VALU kernel (A/B tests)
+  switch (r) {
+#define MW_R(N) case N: return launch_blur_mfma_r<T, N>(in, H, W, C, inv_mean, p, taps, out, st);
+    MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8)
+#undef MW_R
+    default: return MW_EUNSUPPORTED;
+  }
+}
+
+// Fast paths in order: matrix-core kernel, then the VALU register-ring kernel
+// (blur.h); MW_EUNSUPPORTED sends the caller to the two-pass fallback.
+template <typename T>
+int launch_blur_fast(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                     const BlurTaps& taps, int r, float* out, hipStream_t st) {
+  const int rc = launch_blur_mfma<T>(in, H, W, C, inv_mean, p, taps, r, out, st);
+  if (rc != MW_EUNSUPPORTED) return rc;
+  return launch_blur_valu<T>(in, H, W, C, inv_mean, p, taps, r, out, st);
+}
+
+}  // namespace mw

@@ -63,6 +63,15 @@ def main():
     if want("blur"):
         ms = timeit(lambda: D.blur(raw, 2.0, inv_mean=inv, out=blurred), a.reps)
         res["blur"] = (ms, H * W * C * 6, fp(blurred))
+        os.environ["MW_BLUR_IMPL"] = "valu"
+        ref = torch.empty_like(blurred)
+        ms2 = timeit(lambda: D.blur(raw, 2.0, inv_mean=inv, out=ref), a.reps)
+        del os.environ["MW_BLUR_IMPL"]
+        res["blur(valu kernel)"] = (ms2, H * W * C * 6, fp(ref))
+        diff = (blurred - ref).abs()
+        rel = (diff / ref.abs().clamp_min(1e-30)).max().item()
+        print(f"blur mfma vs valu: max abs {diff.max().item():.3e} max rel {rel:.3e}", flush=True)
+        del ref, diff
     # sample rows: S = 0.17 N rows of the blurred slide (fixed random pick)
     S = int(0.17 * H * W)
     g = torch.Generator(device="cuda")
