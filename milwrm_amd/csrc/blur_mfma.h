@@ -60,7 +60,10 @@ template <> struct Chunk16<uint16_t> {
 template <> struct Chunk16<float> {
   static constexpr int P = 2;
   static __device__ __forceinline__ bf2 pair(const u4m& v, int i) {
-    return bf2{__builtin_bit_cast(float, v[2 * i]), __builtin_bit_cast(float, v[2 * i + 1])};
+    // whole-vector bit cast (element-wise casts of vector lanes have been
+    // miscompiled by ROCm 7.2's hipcc: see the staging store in blur history)
+    const f4m f = __builtin_bit_cast(f4m, v);
+    return i == 0 ? bf2{f.x, f.y} : bf2{f.z, f.w};
   }
 };
 

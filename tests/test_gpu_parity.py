@@ -78,6 +78,42 @@ def test_blur_edges_and_fallback_radius(gpu, golden):
         np.testing.assert_allclose(im.img, g[f"gauss{i}_out"], rtol=1e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.float32])
+@pytest.mark.parametrize("shape,sigma", [((70, 131, 30), 2.0), ((37, 64, 16), 1.0),
+                                         ((20, 200, 8), 0.5), ((300, 67, 64), 2.0),
+                                         ((9, 5, 2), 2.0), ((40, 72, 6), 1.5)])
+def test_fused_lognorm_blur_kernels(gpu, dtype, shape, sigma):
+    """Fused log-normalise + blur (matrix-core and VALU fast paths) against the
+    fp64 oracle over input dtypes, channel counts (pad channels, 1-4 channel
+    tiles), radii and band geometries (edge bands, partial last band, images
+    narrower than one band).  Tolerance: fp32 rounding of ~2r+1 products."""
+    import os
+
+    import torch
+
+    from milwrm_amd import device as D
+
+    import zlib
+
+    rng = np.random.default_rng(zlib.crc32(repr((shape, sigma, np.dtype(dtype).str)).encode()))
+    hi = 255 if dtype == np.uint8 else 4000
+    a = rng.integers(0, hi, size=shape).astype(dtype)
+    a[rng.random(shape) < 0.05] = 0
+    inv = (1.0 / rng.uniform(50, 500, size=shape[2])).astype(np.float32)
+    ref = O.gaussian_blur(O.log_normalize(a.astype(np.float64), mean=1.0 / inv.astype(np.float64)),
+                          sigma=sigma)
+    x = D.to_device_image(a)
+    inv_d = torch.from_numpy(inv).cuda()
+    for impl in ("mfma", "valu"):
+        if impl == "valu":
+            os.environ["MW_BLUR_IMPL"] = "valu"
+        try:
+            got = D.blur(x, sigma, inv_mean=inv_d).cpu().numpy()
+        finally:
+            os.environ.pop("MW_BLUR_IMPL", None)
+        np.testing.assert_allclose(got, ref, rtol=2e-6, atol=2e-7, err_msg=impl)
+
+
 def test_downsample(gpu, golden):
     import milwrm_amd as M
 
