@@ -127,6 +127,18 @@ size_t mw_legacy_randint_ws_bytes(int64_t high, int64_t size, int64_t L);
 int mw_legacy_randint_device(uint32_t seed, int64_t high, int64_t size, const uint64_t* d_tables,
                              int J, int64_t L, int32_t* d_out, int64_t* d_total, void* d_ws,
                              void* stream);
+/* The same in two halves.  The segment start states depend only on (seed, L):
+ * every image of a batch reseeds with 16 (MxIF.py:484), so a caller may build
+ * them once (mw_mt_segment_states, W x 624 uint32 in d_states) and draw any
+ * (high, size) needing at most W segments from them
+ * (mw_legacy_randint_from_states; workspace mw_legacy_randint_gen_ws_bytes). */
+int64_t mw_legacy_randint_segments(int64_t high, int64_t size, int64_t L);
+int mw_mt_segment_states(uint32_t seed, int64_t W, const uint64_t* d_tables, int J,
+                         uint32_t* d_states, void* stream);
+size_t mw_legacy_randint_gen_ws_bytes(int64_t high, int64_t size, int64_t L);
+int mw_legacy_randint_from_states(const uint32_t* d_states, int64_t W_avail, int64_t high,
+                                  int64_t size, int64_t L, int32_t* d_out, int64_t* d_total,
+                                  void* d_ws, void* stream);
 
 /* ---- k-means++ (sklearn _kmeans.py:174-272) ---------------------------------
  * Rows are scaled on the fly: x' = (x - mu) * inv_sigma  (fp64 affine).

@@ -48,6 +48,10 @@ _PROTOS = {
     "mw_mt_seed_state": (c_i32, [c_u32, c_vp]),
     "mw_legacy_randint_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "mw_legacy_randint_device": (c_i32, [c_u32, c_i64, c_i64, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "mw_legacy_randint_segments": (c_i64, [c_i64, c_i64, c_i64]),
+    "mw_mt_segment_states": (c_i32, [c_u32, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "mw_legacy_randint_gen_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "mw_legacy_randint_from_states": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mw_kpp_ws_bytes": (c_sz, [c_i64, c_i32]),
     "mw_kpp_init": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "mw_kpp_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),

@@ -227,48 +227,49 @@ size_t mw_legacy_randint_ws_bytes(int64_t high, int64_t size, int64_t L) {
   return (size_t)p.W * kN * 4 + (size_t)p.W * L * 4 + (size_t)(p.W + 1) * 8 + 1024;
 }
 
-int mw_legacy_randint_device(uint32_t seed, int64_t high, int64_t size, const uint64_t* d_tables,
-                             int J, int64_t L, int32_t* d_out, int64_t* d_total, void* d_ws,
-                             void* stream) {
-  MW_CHECK_ARG(d_out && d_total && d_ws, "mw_legacy_randint_device: null pointer");
-  MW_CHECK_ARG(high >= 1 && high <= 2147483648LL && size >= 0, "mw_legacy_randint_device: bad range");
-  MW_CHECK_ARG(L > 0 && L % kN == 0, "mw_legacy_randint_device: L must be a positive multiple of 624");
-  hipStream_t st = as_stream(stream);
-  if (size == 0) {
-    MW_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), st));
-    return MW_OK;
-  }
-  if (high == 1) {  // numpy returns zeros without drawing
-    MW_HIP(hipMemsetAsync(d_out, 0, sizeof(int32_t) * (size_t)size, st));
-    const int64_t s = size;
-    MW_HIP(hipMemcpyAsync(d_total, &s, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    MW_HIP(hipStreamSynchronize(st));
-    return MW_OK;
-  }
-  MW_CHECK_ARG(d_tables != nullptr, "mw_legacy_randint_device: jump tables required");
+int64_t mw_legacy_randint_segments(int64_t high, int64_t size, int64_t L) {
+  if (high < 2 || size <= 0 || L <= 0) return 0;
+  return rng_plan(high, size, L).W;
+}
+
+size_t mw_legacy_randint_gen_ws_bytes(int64_t high, int64_t size, int64_t L) {
+  if (high < 2 || size <= 0 || L <= 0) return 256;
   const RngPlan p = rng_plan(high, size, L);
+  return (size_t)p.W * L * 4 + (size_t)(p.W + 1) * 8 + 1024;
+}
+
+int mw_mt_segment_states(uint32_t seed, int64_t W, const uint64_t* d_tables, int J,
+                         uint32_t* d_states, void* stream) {
+  MW_CHECK_ARG(d_states && d_tables, "mw_mt_segment_states: null pointer");
+  MW_CHECK_ARG(W >= 1 && W <= 1024 * 1024, "mw_mt_segment_states: bad segment count %lld",
+               (long long)W);
   int levels = 0;
-  while ((1ll << levels) < p.W) ++levels;
-  MW_CHECK_ARG(levels <= J, "mw_legacy_randint_device: %lld segments need %d jump levels, tables have %d",
-               (long long)p.W, levels, J);
-  char* base = reinterpret_cast<char*>(d_ws);
-  uint32_t* states = reinterpret_cast<uint32_t*>(base);
-  uint32_t* tmp = states + (size_t)p.W * kN;
-  int64_t* cnt = reinterpret_cast<int64_t*>(tmp + (size_t)p.W * L);
-  hipLaunchKernelGGL(mt_seed_kernel, dim3(1), dim3(64), 0, st, seed, states);
+  while ((1ll << levels) < W) ++levels;
+  MW_CHECK_ARG(levels <= J, "mw_mt_segment_states: %lld segments need %d jump levels, tables have %d",
+               (long long)W, levels, J);
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(mt_seed_kernel, dim3(1), dim3(64), 0, st, seed, d_states);
   MW_LAUNCH_CHECK();
   for (int j = 0; j < levels; ++j) {
     const int64_t half = 1ll << j;
-    const int64_t n = std::min<int64_t>(half, p.W - half);
+    const int64_t n = std::min<int64_t>(half, W - half);
     if (n <= 0) break;
-    hipLaunchKernelGGL(mt_jump_kernel, dim3((unsigned)n), dim3(kRngThreads), 0, st, states, (int)half,
-                       (int)n, d_tables + (size_t)j * kPolyWords);
+    hipLaunchKernelGGL(mt_jump_kernel, dim3((unsigned)n), dim3(kRngThreads), 0, st, d_states,
+                       (int)half, (int)n, d_tables + (size_t)j * kPolyWords);
     MW_LAUNCH_CHECK();
   }
+  return MW_OK;
+}
+
+// generation half: regenerate / temper / filter each segment from its start
+// state, scan the per-segment counts, scatter the first `size` draws
+static int randint_gen(const uint32_t* states, const RngPlan& p, int64_t size, int64_t L,
+                       int32_t* d_out, int64_t* d_total, uint32_t* tmp, int64_t* cnt,
+                       hipStream_t st) {
   hipLaunchKernelGGL(mt_gen_kernel, dim3((unsigned)p.W), dim3(kRngThreads), 0, st, states, L, p.mask,
                      p.rng, tmp, cnt);
   MW_LAUNCH_CHECK();
-  MW_CHECK_ARG(p.W <= 1024 * 1024, "mw_legacy_randint_device: too many segments");
+  MW_CHECK_ARG(p.W <= 1024 * 1024, "mw_legacy_randint: too many segments");
   hipLaunchKernelGGL(mt_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, (int)p.W, d_total);
   MW_LAUNCH_CHECK();
   const unsigned gx = (unsigned)std::min<int64_t>((L + 255) / 256, 64);
@@ -276,6 +277,65 @@ int mw_legacy_randint_device(uint32_t seed, int64_t high, int64_t size, const ui
                      d_total, (int)p.W, L, size, d_out);
   MW_LAUNCH_CHECK();
   return MW_OK;
+}
+
+// numpy's special cases: size 0 draws nothing, high 1 returns zeros
+static int randint_trivial(int64_t high, int64_t size, int32_t* d_out, int64_t* d_total,
+                           hipStream_t st, bool* done) {
+  *done = true;
+  if (size == 0) {
+    MW_HIP(hipMemsetAsync(d_total, 0, sizeof(int64_t), st));
+    return MW_OK;
+  }
+  if (high == 1) {
+    MW_HIP(hipMemsetAsync(d_out, 0, sizeof(int32_t) * (size_t)size, st));
+    const int64_t s = size;
+    MW_HIP(hipMemcpyAsync(d_total, &s, sizeof(int64_t), hipMemcpyHostToDevice, st));
+    MW_HIP(hipStreamSynchronize(st));
+    return MW_OK;
+  }
+  *done = false;
+  return MW_OK;
+}
+
+int mw_legacy_randint_from_states(const uint32_t* d_states, int64_t W_avail, int64_t high,
+                                  int64_t size, int64_t L, int32_t* d_out, int64_t* d_total,
+                                  void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_out && d_total && d_ws, "mw_legacy_randint_from_states: null pointer");
+  MW_CHECK_ARG(high >= 1 && high <= 2147483648LL && size >= 0, "mw_legacy_randint_from_states: bad range");
+  MW_CHECK_ARG(L > 0 && L % kN == 0, "mw_legacy_randint_from_states: L must be a positive multiple of 624");
+  hipStream_t st = as_stream(stream);
+  bool done;
+  const int rc = randint_trivial(high, size, d_out, d_total, st, &done);
+  if (done) return rc;
+  const RngPlan p = rng_plan(high, size, L);
+  MW_CHECK_ARG(d_states && W_avail >= p.W,
+               "mw_legacy_randint_from_states: %lld segment states needed, %lld given",
+               (long long)p.W, (long long)W_avail);
+  uint32_t* tmp = reinterpret_cast<uint32_t*>(d_ws);
+  int64_t* cnt = reinterpret_cast<int64_t*>(tmp + (size_t)p.W * L);
+  return randint_gen(d_states, p, size, L, d_out, d_total, tmp, cnt, st);
+}
+
+int mw_legacy_randint_device(uint32_t seed, int64_t high, int64_t size, const uint64_t* d_tables,
+                             int J, int64_t L, int32_t* d_out, int64_t* d_total, void* d_ws,
+                             void* stream) {
+  MW_CHECK_ARG(d_out && d_total && d_ws, "mw_legacy_randint_device: null pointer");
+  MW_CHECK_ARG(high >= 1 && high <= 2147483648LL && size >= 0, "mw_legacy_randint_device: bad range");
+  MW_CHECK_ARG(L > 0 && L % kN == 0, "mw_legacy_randint_device: L must be a positive multiple of 624");
+  hipStream_t st = as_stream(stream);
+  bool done;
+  const int rc0 = randint_trivial(high, size, d_out, d_total, st, &done);
+  if (done) return rc0;
+  MW_CHECK_ARG(d_tables != nullptr, "mw_legacy_randint_device: jump tables required");
+  const RngPlan p = rng_plan(high, size, L);
+  char* base = reinterpret_cast<char*>(d_ws);
+  uint32_t* states = reinterpret_cast<uint32_t*>(base);
+  uint32_t* tmp = states + (size_t)p.W * kN;
+  int64_t* cnt = reinterpret_cast<int64_t*>(tmp + (size_t)p.W * L);
+  const int rc = mw_mt_segment_states(seed, p.W, d_tables, J, states, stream);
+  if (rc != MW_OK) return rc;
+  return randint_gen(states, p, size, L, d_out, d_total, tmp, cnt, st);
 }
 
 }  // extern "C"

@@ -72,10 +72,41 @@ def subsample_indices_device(M: int, fract: float, random_state: int = 16, devic
         return out, total
     if M > 2**31:
         raise NotImplementedError("subsample over more than 2^31 masked pixels")
-    ws = D.WS.get("mtrng", N.query("mw_legacy_randint_ws_bytes", int(M), S, MT_SEGMENT))
-    N.call("mw_legacy_randint_device", int(random_state) & 0xFFFFFFFF, int(M), S,
-           D.P(_jump_tables(dev)), MT_LEVELS, MT_SEGMENT, D.P(out), D.P(total), D.P(ws), D.stream())
+    seed = int(random_state) & 0xFFFFFFFF
+    W = N.query("mw_legacy_randint_segments", int(M), S, MT_SEGMENT)
+    states, W_avail = _segment_states(dev, seed, W)
+    ws = D.WS.get("mtrng", N.query("mw_legacy_randint_gen_ws_bytes", int(M), S, MT_SEGMENT))
+    N.call("mw_legacy_randint_from_states", D.P(states), W_avail, int(M), S, MT_SEGMENT, D.P(out),
+           D.P(total), D.P(ws), D.stream())
     return out, total
+
+
+_states = {}
+
+
+def _segment_states(dev, seed: int, W: int):
+    """MT19937 start states of the first >= W stream segments for ``seed``
+    (a pure function of (seed, MT_SEGMENT)), built on the device by the jump
+    prefix and memoised per (device, seed): every image reseeds with the same
+    constant (MxIF.py:484), so the jumps run once per process, not per image.
+    Grown to the next power of two when a larger draw needs more segments."""
+    import torch
+
+    from . import _native as N
+    from . import device as D
+
+    key = (str(dev), seed)
+    hit = _states.get(key)
+    if hit is not None and hit[1] >= W:
+        return hit
+    W_new = 1 << max(0, int(W - 1).bit_length())
+    if hit is not None:
+        W_new = max(W_new, 2 * hit[1])
+    states = torch.empty(W_new * 624, dtype=torch.int32, device=dev)
+    N.call("mw_mt_segment_states", seed, W_new, D.P(_jump_tables(dev)), MT_LEVELS, D.P(states),
+           D.stream())
+    _states[key] = (states, W_new)
+    return _states[key]
 
 
 def check_total(total, S: int):
