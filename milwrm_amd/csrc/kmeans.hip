@@ -73,13 +73,33 @@ __device__ __forceinline__ void wt_tail(int nfl, int64_t e0, int64_t n4, const f
   }
 }
 
+// ---- wave-tile streaming with buffer loads: the resource covers a block's
+// rows from its first row to the end of the array (32-bit block-relative
+// offsets, hardware range check), the tile offset is a scalar (tile index is
+// wave-uniform) and the per-lane offsets are constants, so a tile fetch costs
+// no VALU.  Loads past the end return 0; stores past the range are dropped.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
+  const uint64_t n = nbytes < 0 ? 0 : (uint64_t)nbytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(uint32_t)(n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull),
+                                           0x00020000);
+}
+template <int NV>
+__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t rs, int soff, int lane, f4v (&v)[NV]) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + i * 1024, soff, 0));
+}
+
+constexpr int kKppTab = 64 * 9;  // doubles: k-means++ candidate table inv[64] | b[64][8]
+
 // ===================================================================== kpp
 // Workspace layout (bytes, 256-aligned sections):
 //   bank[2][T][S] fp64  candidate-min distance arrays (ping-pong per step)
 //   bsum[2][T][G] fp64  their per-block sums
 //   st: cand[T] i64, chosen[256] i64, best i32
 struct KppLayout {
-  size_t bank, bsum, st, total;
+  size_t bank, bsum, st, tab, total;
   int G;
 };
 static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -89,7 +109,8 @@ static KppLayout kpp_layout(int64_t S, int T) {
   L.bank = 0;
   L.bsum = al256(L.bank + 2 * (size_t)T * S * sizeof(double));
   L.st = al256(L.bsum + 2 * (size_t)T * L.G * sizeof(double));
-  L.total = al256(L.st + (size_t)(T + 256) * sizeof(int64_t) + 64);
+  L.tab = al256(L.st + (size_t)(T + 256) * sizeof(int64_t) + 64);
+  L.total = al256(L.tab + (size_t)kKppTab * sizeof(double));
   return L;
 }
 struct KppState {
@@ -237,65 +258,71 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(const double* __restri
   }
 }
 
+// k-means++ candidate table (one per distance pass): w_tf = x_f * inv_f - b_tf
+// with b_tf = mu_f * inv_f + c_tf, c_t the scaled candidate rows (from `rows`,
+// T x F floats, or X[cand[t]]); padded features get inv = b = 0.  Stored
+// feature-major [f][8] so the distance pass reads it with uniform (scalar)
+// loads.
+__global__ void __launch_bounds__(512) kpp_prep_kernel(const float* __restrict__ X, int F,
+                                                       const double* __restrict__ mu,
+                                                       const double* __restrict__ inv,
+                                                       const int64_t* __restrict__ cand,
+                                                       const float* __restrict__ rows, int T,
+                                                       double* __restrict__ tab,
+                                                       int64_t* __restrict__ chosen_reset) {
+  const int q = threadIdx.x;  // 512 = 64 features x 8 candidates
+  const int f = q >> 3, c = q & 7;
+  double bv = 0.0;
+  if (f < F && c < T) {
+    const float xv = rows ? rows[c * F + f] : X[cand[c] * F + f];
+    const double cs = ((double)xv - mu[f]) * inv[f];
+    bv = fma(mu[f], inv[f], cs);
+  }
+  tab[64 + f * 8 + c] = bv;
+  if (c == 0) tab[f] = f < F ? inv[f] : 0.0;
+  if (chosen_reset && q == 0) chosen_reset[0] = -1;
+}
+
 // Distance pass of k-means++ (sklearn _kmeans_plusplus, _kmeans.py:225-260):
-// fp64 squared distances of every row to T candidate rows (scaled on the fly,
-// same FMA order as a sequential per-feature loop), elementwise min with the
-// current closest distances cur = bank_prev[best] (init: no min), written to
-// bank_new[t], plus per-block sums.  Candidate rows come from `rows`
-// (T x F floats, host-gathered or the first center) or X[cand[t]].
-// Waves stream 64-row tiles with the next tile's loads in flight (as Lloyd).
-template <int FMAX>
+// fp64 squared distances of every row to T candidate rows, w = fma(x, inv,
+// -b) per feature (the scaler folded in, one rounding) and T independent FMA
+// chains (features in order), elementwise min with the current closest
+// distances cur = bank_prev[best] (init: no min), written to bank_new[t],
+// plus per-block sums.  Waves stream 64-row tiles (buffer loads, next tile in
+// flight); the candidate table comes through scalar loads.
+template <int FMAX, int T>
 __global__ void __launch_bounds__(256, MW_KPP_WPS) kpp_dist_kernel(
-    const float* __restrict__ X, int64_t S, int F, const double* __restrict__ mu,
-    const double* __restrict__ inv, const double* __restrict__ bank_prev,
-    const int* __restrict__ best, int best_val, const int64_t* __restrict__ cand,
-    const float* __restrict__ rows, int T, int64_t R, double* __restrict__ bank_new,
-    double* __restrict__ bsum_new, int64_t* __restrict__ chosen_reset) {
+    const float* __restrict__ X, int64_t S, int F, const double* __restrict__ tab,
+    const double* __restrict__ bank_prev, const int* __restrict__ best, int best_val, int64_t R,
+    double* __restrict__ bank_new, double* __restrict__ bsum_new) {
   constexpr int NV = FMAX / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ double s_c[8 * FMAX];
-  __shared__ double s_mu[FMAX], s_inv[FMAX];
   __shared__ double s_red[4];
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
+  const int t = threadIdx.x, lane = t & 63, nw = blockDim.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   float* s_tile = reinterpret_cast<float*>(smem) + (size_t)wid * 64 * FMAX;
-  for (int f = t; f < FMAX; f += blockDim.x) {
-    s_mu[f] = f < F ? mu[f] : 0.0;  // padded features scale to exactly 0
-    s_inv[f] = f < F ? inv[f] : 0.0;
-  }
-  for (int q = t; q < 8 * FMAX; q += blockDim.x) {
-    const int c = q / FMAX, f = q - c * FMAX;
-    double v = 0.0;
-    if (c < T && f < F) {
-      const float xv = rows ? rows[c * F + f] : X[cand[c] * F + f];
-      v = ((double)xv - mu[f]) * inv[f];
-    }
-    s_c[q] = v;
-  }
-  if (chosen_reset && blockIdx.x == 0 && t == 0) chosen_reset[0] = -1;
-  const double* cur = bank_prev ? bank_prev + (size_t)(best ? *best : best_val) * S : nullptr;
-  __syncthreads();
+  const bool has_cur = bank_prev != nullptr;
+  const double* cur = has_cur ? bank_prev + (size_t)(best ? *best : best_val) * S : nullptr;
 
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
   const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
   const int64_t total = S * (int64_t)F, n4 = total >> 2;
-  const f4v* X4 = reinterpret_cast<const f4v*>(X);
-  double acc[8];
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + lo * F, (S - lo) * F * 4);
+  const __amdgpu_buffer_rsrc_t rc =
+      make_rsrc(has_cur ? static_cast<const void*>(cur + lo) : static_cast<const void*>(X),
+                has_cur ? (hi - lo) * 8 : 0);
+  const int tile_bytes = 64 * F * 4;
+  double acc[T];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c] = 0.0;
+  for (int c = 0; c < T; ++c) acc[c] = 0.0;
 
   f4v v[NV];
   double cur_next = 0.0;
   auto fetch = [&](int tt) {
     tt = tt < ntile ? tt : ntile - 1;
-    const int64_t r = lo + (int64_t)tt * 64;
-    if (cur) cur_next = cur[min(r + lane, hi - 1)];
-    const int64_t q0 = (r * F) >> 2;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      int64_t q = q0 + lane + i * 64;
-      q = q < n4 ? q : n4 - 1;
-      v[i] = X4[q];
-    }
+    if (has_cur)
+      cur_next = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, lane * 8, tt * 512, 0));
+    tile_load<NV>(rx, tt * tile_bytes, lane, v);
   };
   int tc = wid;
   if (tc < ntile) fetch(tc);
@@ -310,42 +337,36 @@ __global__ void __launch_bounds__(256, MW_KPP_WPS) kpp_dist_kernel(
     wt_tail(nrow * F, r0 * F, n4, X, total, s_tile, lane);
     const double cd = cur_next;
     fetch(tc + nw);
-    // launder the LDS bases so the per-feature constants are re-read per tile
-    // instead of being pinned in registers across the loop
-    int z = 0;
-    asm volatile("" : "+s"(z));
-    const double* smu = s_mu + z;
-    const double* sinv = s_inv + z;
-    const double* sc = s_c + z;
-    double xs[FMAX];
     const float* xr = s_tile + lane * F;
+    const double* tb = tab;  // uniform: hipcc keeps the table in SGPRs/VGPRs
+    double d[T];
 #pragma unroll
-    for (int f = 0; f < FMAX; ++f) xs[f] = ((double)xr[f] - smu[f]) * sinv[f];
+    for (int c = 0; c < T; ++c) d[c] = 0.0;
+#pragma unroll
+    for (int f = 0; f < FMAX; ++f) {
+      const double xd = (double)xr[f];  // features past F: inv = b = 0 (rows finite)
+      const double iv = tb[f];
+#pragma unroll
+      for (int c = 0; c < T; ++c) {
+        const double w = fma(xd, iv, -tb[64 + f * 8 + c]);
+        d[c] = fma(w, w, d[c]);
+      }
+    }
     const bool valid = lane < nrow;
     const int64_t row = r0 + lane;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      if (c < T) {
-        double d = 0.0;
-#pragma unroll
-        for (int f = 0; f < FMAX; ++f) {
-          const double w = xs[f] - sc[c * FMAX + f];
-          d = fma(w, w, d);
-        }
-        const double m = (cur && cd < d) ? cd : d;
-        if (valid) {
-          bank_new[(size_t)c * S + row] = m;
-          acc[c] += m;
-        }
+    for (int c = 0; c < T; ++c) {
+      const double m = (has_cur && cd < d[c]) ? cd : d[c];
+      if (valid) {
+        bank_new[(size_t)c * S + row] = m;
+        acc[c] += m;
       }
     }
   }
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    if (c < T) {
-      const double tot = block_sum(acc[c], s_red);
-      if (t == 0) bsum_new[(size_t)c * gridDim.x + blockIdx.x] = tot;
-    }
+  for (int c = 0; c < T; ++c) {
+    const double tot = block_sum(acc[c], s_red);
+    if (t == 0) bsum_new[(size_t)c * gridDim.x + blockIdx.x] = tot;
   }
 }
 
@@ -502,24 +523,6 @@ __host__ __device__ inline size_t lloyd_wave_bytes(int FMAX) { return (size_t)64
 // pair-major center image (FMAX/2 x kpad4(k) float pairs)
 __host__ __device__ inline size_t cent_t_bytes(int KS, int FMAX) {
   return (size_t)(FMAX / 2) * KS * 8;
-}
-
-// ---- wave-tile streaming with buffer loads: the resource covers a block's
-// rows from its first row to the end of the array (32-bit block-relative
-// offsets, hardware range check), the tile offset is a scalar (tile index is
-// wave-uniform) and the per-lane offsets are constants, so a tile fetch costs
-// no VALU.  Loads past the end return 0; stores past the range are dropped.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
-  const uint64_t n = nbytes < 0 ? 0 : (uint64_t)nbytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
-                                           (int)(uint32_t)(n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull),
-                                           0x00020000);
-}
-template <int NV>
-__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t rs, int soff, int lane, f4v (&v)[NV]) {
-#pragma unroll
-  for (int i = 0; i < NV; ++i)
-    v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + i * 1024, soff, 0));
 }
 
 // One Lloyd pass (lloyd_iter_chunked_dense, _k_means_lloyd.pyx:23-218):
@@ -971,22 +974,33 @@ static KppPtrs kpp_ptrs(const void* d_ws, int64_t S, int T) {
   return p;
 }
 
-// launch the distance pass with the FMAX instance for F
+// candidate table, then the distance pass with the (FMAX, T) instance
 static int kpp_dist_launch(const float* X, int64_t S, int F, const double* mu, const double* inv,
                            const double* bank_prev, const int* best, int best_val,
                            const int64_t* cand, const float* rows, int T, const KppLayout& L,
-                           double* bank_new, double* bsum_new, int64_t* chosen_reset,
+                           char* ws, double* bank_new, double* bsum_new, int64_t* chosen_reset,
                            hipStream_t s) {
+  double* tab = reinterpret_cast<double*>(ws + L.tab);
+  hipLaunchKernelGGL(kpp_prep_kernel, dim3(1), dim3(512), 0, s, X, F, mu, inv, cand, rows, T, tab,
+                     chosen_reset);
+  MW_LAUNCH_CHECK();
   const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
   const size_t lds = (size_t)4 * 64 * FM * sizeof(float);
-#define MW_KD(FMV)                                                                              \
-  hipLaunchKernelGGL(kpp_dist_kernel<FMV>, dim3(L.G), dim3(256), lds, s, X, S, F, mu, inv,     \
-                     bank_prev, best, best_val, cand, rows, T, krows(S), bank_new, bsum_new,    \
-                     chosen_reset)
-  if (FM == 8) MW_KD(8);
-  else if (FM == 16) MW_KD(16);
-  else if (FM == 32) MW_KD(32);
-  else MW_KD(64);
+#define MW_KD(FMV, TV)                                                                          \
+  hipLaunchKernelGGL((kpp_dist_kernel<FMV, TV>), dim3(L.G), dim3(256), lds, s, X, S, F, tab,   \
+                     bank_prev, best, best_val, krows(S), bank_new, bsum_new)
+#define MW_KDT(FMV)                                                                  \
+  switch (T) {                                                                       \
+    case 1: MW_KD(FMV, 1); break; case 2: MW_KD(FMV, 2); break;                      \
+    case 3: MW_KD(FMV, 3); break; case 4: MW_KD(FMV, 4); break;                      \
+    case 5: MW_KD(FMV, 5); break; case 6: MW_KD(FMV, 6); break;                      \
+    case 7: MW_KD(FMV, 7); break; default: MW_KD(FMV, 8); break;                     \
+  }
+  if (FM == 8) { MW_KDT(8) }
+  else if (FM == 16) { MW_KDT(16) }
+  else if (FM == 32) { MW_KDT(32) }
+  else { MW_KDT(64) }
+#undef MW_KDT
 #undef MW_KD
   MW_LAUNCH_CHECK();
   return MW_OK;
@@ -999,8 +1013,8 @@ int mw_kpp_init(const float* d_X, int64_t S, int F, const double* d_mu, const do
   MW_CHECK_ARG(T >= 1 && T <= 8, "mw_kpp_init: n_local_trials must be in [1, 8]");
   const KppPtrs p = kpp_ptrs(d_ws, S, T);
   return kpp_dist_launch(d_X, S, F, d_mu, d_inv, nullptr, nullptr, 0, nullptr, d_center_row, 1,
-                         p.L, p.bank_of(0, T, S), p.bsum_of(0, T), p.st.chosen,
-                         as_stream(stream));
+                         p.L, static_cast<char*>(d_ws), p.bank_of(0, T, S), p.bsum_of(0, T),
+                         p.st.chosen, as_stream(stream));
 }
 
 int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu, const double* d_inv, int c,
@@ -1020,7 +1034,8 @@ int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu, const do
                      (const double*)nullptr);
   MW_LAUNCH_CHECK();
   return kpp_dist_launch(d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S), p.st.best, 0, p.st.cand,
-                         nullptr, T, p.L, p.bank_of(c, T, S), p.bsum_of(c, T), nullptr, s);
+                         nullptr, T, p.L, static_cast<char*>(d_ws), p.bank_of(c, T, S),
+                         p.bsum_of(c, T), nullptr, s);
 }
 
 int mw_kpp_indices(const void* d_ws, int64_t S, int T, int k, int64_t* d_idx_out, void* stream) {
@@ -1070,8 +1085,8 @@ int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu, const d
                "mw_kpp_trial: bad args");
   const KppPtrs p = kpp_ptrs(d_ws, S, T);
   return kpp_dist_launch(d_X, S, F, d_mu, d_inv, p.bank_of(c - 1, T, S), nullptr, best, nullptr,
-                         d_rows, T, p.L, p.bank_of(c, T, S), p.bsum_of(c, T), nullptr,
-                         as_stream(stream));
+                         d_rows, T, p.L, static_cast<char*>(d_ws), p.bank_of(c, T, S),
+                         p.bsum_of(c, T), nullptr, as_stream(stream));
 }
 
 size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
