@@ -102,6 +102,33 @@ size_t mw_gather_ws_bytes(int64_t S, int F);
 int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F,
                    const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S,
                    float* d_X, void* d_ws, void* stream);
+/* Column statistics of rows already in X (same per-block records as
+ * mw_gather_rows, same order: identical numbers for identical rows); then
+ * mw_col_stats_finalize. */
+int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stream);
+
+/* ---- fused blur + subsample (MxIF.py:375-394 + 457-492, MILWRM.py:1716-1733)
+ * The subsample rows are written by the blur itself, so the blurred slide is
+ * never stored:
+ *   mw_sample_map:   head[p] = smallest j with rank2pix[idx[j]] == p (INT32 max
+ *                    if none; d_head holds mw_sample_head_elems(n_pix) int32),
+ *                    pix[j] = rank2pix[idx[j]];
+ *   mw_blur_sample:  lognorm + blur of the slide; X[head[p], f] =
+ *                    blurred[p, feat[f]] for every sampled pixel p;
+ *   mw_sample_fixup: X[j] = X[head[pix[j]]] for the repeated draws;
+ * then mw_col_stats_rows.  X ends up equal to mw_blur + mw_gather_rows.
+ * mw_blur_sample returns MW_EUNSUPPORTED (nothing launched) for shapes the
+ * fused kernel does not take (odd C, C > 64, radius 0 or > 8, F > C rounded
+ * up to 16, no log-normalise); the caller then materialises the blur. */
+size_t mw_sample_head_elems(int64_t n_pix);
+int mw_sample_map(const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S, int64_t n_pix,
+                  int32_t* d_head, int32_t* d_pix, void* stream);
+int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
+                   float pseudoval, const float* h_weights, int radius, const int32_t* d_head,
+                   int64_t S, const int32_t* d_feat, int F, float* d_X, void* stream);
+int mw_sample_fixup(const int32_t* d_pix, const int32_t* d_head, int64_t S, int F, float* d_X,
+                    void* stream);
+
 /* Chan-merge the per-block stats of the last gather(s) into d_stats =
  * [n, mean[F], M2[F]] (fp64).  `n_parts` gathers may be accumulated: pass
  * the workspace of each; merged in call order. */
@@ -207,6 +234,19 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F,
                    const float* d_a, const float* d_b, const float* d_centers,
                    int k, const uint8_t* d_mask, int64_t n_pix,
                    int8_t* d_label, float* d_conf, void* d_ws, void* stream);
+/* Fused blur + label/confidence (features = all C channels in order): the
+ * same labels and confidences as mw_blur then mw_assign_conf, without the
+ * blurred slide in HBM; k <= 16 (k <= 8 for C <= 16).  d_mask must be
+ * readable 128 bytes past n_pix.  MW_EUNSUPPORTED (nothing launched) as for
+ * mw_blur_sample.  mw_domain_records then writes mw_assign_conf's per-block
+ * records from the label/confidence maps (same partition and order), for
+ * mw_assign_reduce. */
+int mw_blur_assign_conf(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
+                        float pseudoval, const float* h_weights, int radius, const float* d_a,
+                        const float* d_b, const float* d_centers, int k, const uint8_t* d_mask,
+                        int8_t* d_label, float* d_conf, void* stream);
+int mw_domain_records(const int8_t* d_label, const float* d_conf, int64_t n_pix, int C, int k,
+                      void* d_ws, void* stream);
 int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom,
                      void* stream);
 

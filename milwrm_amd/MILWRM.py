@@ -22,7 +22,7 @@ import pandas as pd
 import torch
 
 from . import device as D
-from .assign import assign_image, assign_rows, domain_means
+from .assign import assign_image, assign_rows, blur_assign_image, domain_means
 from .kmeans import DeviceRows, KMeans, StandardScaler
 from .MxIF import checktype, img
 from .ST import blur_features_st
@@ -137,9 +137,31 @@ def estimate_confidence_score_st(sub_cluster_data, adata, centroids):
 def _assign_img(image: img, features, centers, scaler):
     feats = image._features(features)
     mu, inv = scaler.affine()
+    if image._pending_blur is not None and feats == list(range(image.n_ch)):
+        # deferred blur (D.defer_blur): label + confidence straight from the
+        # raw slide, the blurred slide is recomputed in registers and LDS
+        sigma, truncate = image._pending_blur
+        inv_mean, p = image._pending
+        res = blur_assign_image(image._device(), sigma, inv_mean, p, mu, inv,
+                                np.asarray(centers, dtype=np.float64), image._mask_device(),
+                                truncate=truncate)
+        if res is not None:
+            return res
     src = D.as_float32(image._materialize())
     return assign_image(src, feats, mu, inv, np.asarray(centers, dtype=np.float64),
                         image._mask_device())
+
+
+def _gather_deferred(image: img, feat, idx, r2p, X_out) -> bool:
+    """Subsample rows written by the blur itself for an image whose blur is
+    deferred (D.defer_blur); False when it is not, or the fused kernel does
+    not take the shape (the caller materialises and gathers)."""
+    if image._pending_blur is None:
+        return False
+    sigma, truncate = image._pending_blur
+    inv_mean, p = image._pending
+    return D.blur_gather_fused(image._device(), sigma, inv_mean, p, feat, idx, r2p, X_out,
+                               truncate=truncate)
 
 
 def _labels_to_host(lab: torch.Tensor) -> np.ndarray:
@@ -334,8 +356,11 @@ class mxif_labeler(tissue_labeler):
                 idx, tot = subsample_indices_device(M, fract, 16, dev)
                 totals.append((tot, S))
                 feat = D.h2d(np.asarray(im._features(features), dtype=np.int32), dev)
-                D.gather_rows(D.as_float32(im._device()), feat, idx, r2p, X[off:off + S], stats,
-                              accumulate=off > 0)
+                if _gather_deferred(im, feat, idx, r2p, X[off:off + S]):
+                    D.col_stats_rows(X[off:off + S], stats, accumulate=off > 0)
+                else:
+                    D.gather_rows(D.as_float32(im._materialize()), feat, idx, r2p, X[off:off + S],
+                                  stats, accumulate=off > 0)
             off += S
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))

@@ -63,6 +63,7 @@ class img:
         self._host64 = None
         self._dev = None            # HWC device tensor (authoritative when set)
         self._pending = None        # (inv_mean fp32 device tensor, pseudoval) deferred log_normalize
+        self._pending_blur = None   # (sigma, truncate) deferred gaussian (fused-epilogue mode)
         self.n_ch = img_arr.shape[2] if img_arr.ndim > 2 else 1
         if channels is None:
             self.ch = ["ch_{}".format(x) for x in range(self.n_ch)]
@@ -91,7 +92,15 @@ class img:
         return self._dev
 
     def _materialize(self) -> torch.Tensor:
-        """Apply a deferred log_normalize (standalone kernel)."""
+        """Apply a deferred blur (with its log_normalize fused) or a deferred
+        log_normalize (standalone kernel)."""
+        if self._pending_blur is not None:
+            sigma, truncate = self._pending_blur
+            inv, p = self._pending
+            self._pending_blur = None
+            self._pending = None
+            self._set_device(D.blur(self._device(), sigma, inv_mean=inv, pseudoval=p,
+                                    truncate=truncate))
         if self._pending is not None:
             inv, p = self._pending
             self._pending = None
@@ -108,7 +117,7 @@ class img:
     def img(self) -> np.ndarray:
         """The reference's float64 HWC array (materialised from HBM on read)."""
         if self._host64 is None:
-            if self._dev is None and self._pending is None:
+            if self._dev is None and self._pending is None and self._pending_blur is None:
                 self._host64 = self._host.astype("float64")
             else:
                 t = self._materialize()
@@ -124,6 +133,7 @@ class img:
         self._host64 = None
         self._dev = None
         self._pending = None
+        self._pending_blur = None
 
     @property
     def mask(self):
@@ -139,7 +149,7 @@ class img:
             if self._mask is None:
                 raise AssertionError("No tissue mask available")
             m = np.ascontiguousarray(np.asarray(self._mask) != 0, dtype=np.uint8)
-            self._mask_dev = torch.from_numpy(m).to(D.device())
+            self._mask_dev = D.padded_mask(torch.from_numpy(m).to(D.device()))
         return self._mask_dev
 
     # -------------------------------------------------------------- basics
@@ -192,6 +202,7 @@ class img:
         obj._host64 = None
         obj._dev = tensor
         obj._pending = None
+        obj._pending_blur = None
         obj.n_ch = int(tensor.shape[2])
         obj.ch = channels if channels is not None else ["ch_{}".format(x) for x in range(obj.n_ch)]
         obj._mask = None
@@ -268,7 +279,13 @@ class img:
             if mode != "nearest" or kwargs:
                 raise NotImplementedError(f"gaussian options {dict(mode=mode, **kwargs)} "
                                           "(only mode='nearest' is implemented)")
-            src = self._device()
+            src = self._materialize() if self._pending_blur is not None else self._device()
+            if self._pending is not None and src.dim() == 3 and D.defer_blur(*src.shape):
+                # fused-epilogue mode: the subsample gather and the label pass
+                # recompute the blur from the raw slide (D.defer_blur)
+                self._pending_blur = (float(sigma), truncate)
+                self._host64 = None
+                return
             inv, p = self._pending if self._pending is not None else (None, 1.0)
             self._pending = None
             out = D.blur(src, float(sigma), inv_mean=inv, pseudoval=p, truncate=truncate)
@@ -374,7 +391,7 @@ class img:
         var = stats[1 + F:] / stats[0]
         km = KMeans(n_clusters=2, random_state=18).fit(DeviceRows(X, feature_var=var))
         feats = cp._features(features)
-        lab, _, _ = assign_image(cp._device(), feats, np.zeros(F), np.ones(F), km.cluster_centers_,
+        lab, _, _ = assign_image(D.as_float32(cp._materialize()), feats, np.zeros(F), np.ones(F), km.cluster_centers_,
                                  cp._mask_device())
         tID = lab.cpu().numpy().astype(float)
         scores = km.cluster_centers_

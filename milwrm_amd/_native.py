@@ -67,6 +67,13 @@ _PROTOS = {
     "mw_assign_ws_bytes": (c_sz, [c_i64, c_i32]),
     "mw_assign_conf": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_reduce": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_col_stats_rows": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_sample_head_elems": (c_sz, [c_i64]),
+    "mw_sample_map": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "mw_blur_sample": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "mw_sample_fixup": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_blur_assign_conf": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mw_domain_records": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mw_synth_slide": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_u64, c_vp, c_vp, c_vp]),
 }
 
@@ -117,6 +124,17 @@ def call(name: str, *args):
     """Invoke ``name`` and raise on a non-zero status."""
     fn = getattr(load(), name)
     check(fn(*args), name)
+
+
+def try_call(name: str, *args) -> bool:
+    """Invoke ``name``; False when it reports MW_EUNSUPPORTED (nothing was
+    launched: the caller takes its materialising path), raise on any other
+    non-zero status."""
+    st = getattr(load(), name)(*args)
+    if st == _EUNSUP:
+        return False
+    check(st, name)
+    return True
 
 
 def query(name: str, *args) -> int:

@@ -38,6 +38,43 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
     return lab, conf, dom
 
 
+def blur_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: float, mu, inv,
+                      centers: np.ndarray, mask_u8: torch.Tensor, truncate: float = 4.0):
+    """``assign_image(blur(lognorm(raw)), all channels, ...)`` in one pass over
+    the raw slide (the fused blur assign epilogue; the blurred slide is never
+    stored), then the same per-block domain records.  None when the fused
+    kernel does not take this shape (the caller materialises the blur)."""
+    H, W, C = raw.shape
+    k, F = centers.shape
+    if F != C or inv_mean is None:
+        return None
+    dev = raw.device
+    a = D.h2d(np.asarray(inv, dtype=np.float64).astype(np.float32), dev)
+    b = D.h2d((-np.asarray(mu, dtype=np.float64) * np.asarray(inv, dtype=np.float64))
+              .astype(np.float32), dev)
+    c32 = D.h2d(np.asarray(centers, dtype=np.float32), dev)
+    w = D.gaussian_taps(sigma, truncate)
+    r = (len(w) - 1) // 2
+    n = H * W
+    lab = torch.empty((H, W), dtype=torch.int8, device=dev)
+    conf = torch.empty((H, W), dtype=torch.float32, device=dev)
+    mask_u8 = D.padded_mask(mask_u8)
+    st = D.stream()
+    with profiling.timed("blur_assign", n * (C * raw.element_size() + 5)):
+        ok = N.try_call("mw_blur_assign_conf", D.P(raw), D.dtype_code(raw), H, W, C, D.P(inv_mean),
+                        float(pseudoval), w.ctypes.data, r, D.P(a), D.P(b), D.P(c32), k,
+                        D.P(mask_u8), D.P(lab), D.P(conf), st)
+    if not ok:
+        return None
+    D.FUSED_USED["assign"] += 1
+    dom = torch.empty(2 * k, dtype=torch.float64, device=dev)
+    ws = D.WS.get("assign", N.query("mw_assign_ws_bytes", n, k))
+    with profiling.timed("domain_records", n * 5):
+        N.call("mw_domain_records", D.P(lab), D.P(conf), n, C, k, D.P(ws), st)
+    N.call("mw_assign_reduce", D.P(ws), n, k, D.P(dom), st)
+    return lab, conf, dom
+
+
 def assign_rows(X: np.ndarray, centers: np.ndarray, mu=None, inv=None):
     """Assign host rows (S x F, already in the centers' space unless an
     affine is given).  Returns (labels int64, conf fp64, dom fp64[2k])."""

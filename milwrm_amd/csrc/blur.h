@@ -38,6 +38,35 @@ typedef float bf2 __attribute__((ext_vector_type(2)));
 template <typename T>
 int launch_blur_fast(const T* in, int H, int W, int C, const float* inv_mean, float p,
                      const struct BlurTaps& taps, int r, float* out, hipStream_t st);
+constexpr int kEpiStore = 0, kEpiSample = 1, kEpiAssign = 2;
+constexpr int kEpiKS = 16;  // assign epilogue: center stride (k <= 2 * threads per column)
+
+struct BlurEpi {
+  const int32_t* head;     // kEpiSample: n_pix + 128 slots (int32 max: no sample)
+  int64_t S;               //   rows of X
+  float* X;                //   S x F
+  int F;
+  const int32_t* feat;     //   F channel indices (device)
+  const uint8_t* mask;     // kEpiAssign: nonzero = tissue (readable 128 B past the end)
+  int8_t* lab;             //   label per pixel (-1 outside the mask)
+  float* conf;             //   confidence per pixel (NaN outside the mask)
+  const float* a;          //   scaler per channel (features = all channels in order)
+  const float* b;
+  const float* centers;    //   k x C, scaled space
+  int k;
+};
+
+template <typename T>
+int launch_blur_epi(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                    const struct BlurTaps& taps, int r, const BlurEpi& ep, int epi, hipStream_t st);
+
+// 1/v to ~12% from the exponent/mantissa bits (one integer subtract): the
+// factor of the rounding-error correction below, whose size is at most half
+// an ulp of v — a 12% error there moves the result by < 2^-27 relative, and
+// saves the quarter-rate v_rcp_f32 per element
+__device__ __forceinline__ float rcp_coarse(float v) {
+  return __builtin_bit_cast(float, 0x7EF311C3u - __builtin_bit_cast(uint32_t, v));
+}
 
 // accurate log10(t + p) for t >= 0 (log1p-style correction of the rounding
 // of t + p, so small t keep full relative accuracy)
@@ -46,7 +75,7 @@ __device__ __forceinline__ float lognorm1(float x, float inv, float p) {
   const float v = t + p;
   const float e = (v - p) - t;  // rounding error of t + p (exact)
   const float l2 = __builtin_amdgcn_logf(v);  // log2, 1 ulp
-  return l2 * 0.30102999566398120f - (e * __builtin_amdgcn_rcpf(v)) * 0.43429448190325182f;
+  return l2 * 0.30102999566398120f - (e * rcp_coarse(v)) * 0.43429448190325182f;
 }
 
 // the same on an element pair with packed arithmetic (v_pk_*; the two
@@ -57,7 +86,7 @@ __device__ __forceinline__ bf2 lognorm2(bf2 x, bf2 inv, float p) {
   const bf2 v = t + pp;
   const bf2 e = (v - pp) - t;
   const bf2 l2 = bf2{__builtin_amdgcn_logf(v.x), __builtin_amdgcn_logf(v.y)};
-  const bf2 rv = bf2{__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)};
+  const bf2 rv = bf2{rcp_coarse(v.x), rcp_coarse(v.y)};
   return __builtin_elementwise_fma(l2, bf2{0.30102999566398120f, 0.30102999566398120f},
                                    (e * rv) * bf2{-0.43429448190325182f, -0.43429448190325182f});
 }
@@ -304,8 +333,12 @@ int launch_blur_valu(const T* in, int H, int W, int C, const float* inv_mean, fl
   if (C % 2 != 0 || C > 64 || r < 0 || r > kBlurMaxR) return MW_EUNSUPPORTED;
   switch (r) {
 #define MW_R(N) case N: return launch_blur_r<T, N>(in, H, W, C, inv_mean, p, taps, out, st);
+#ifdef MW_BLUR_DEV
+    MW_R(8)
+#else
     MW_R(0) MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8) MW_R(9) MW_R(10)
     MW_R(11) MW_R(12)
+#endif
 #undef MW_R
     default: return MW_EUNSUPPORTED;
   }

@@ -37,6 +37,7 @@ constexpr int kBlurMfmaMaxR = 8;
 
 typedef float f4m __attribute__((ext_vector_type(4)));
 typedef unsigned int u4m __attribute__((ext_vector_type(4)));
+typedef float f2m_ __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t blur_rsrc(const void* base, uint32_t nbytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
@@ -100,7 +101,20 @@ __device__ __forceinline__ void vm_wait_n() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename T, int R, int CT, int BT>
+// What happens to an output row once the vertical pass has staged it in LDS:
+//   kEpiStore   store the blurred row (HWC fp32): img.blurring
+//   kEpiSample  write the subsample rows straight from the blur: pixel p's
+//               features go to X[head[p]] (head = smallest sample slot of p,
+//               mw_sample_map; the other slots of p are copied afterwards)
+//   kEpiAssign  StandardScaler + nearest center + confidence per pixel
+//               (KMeans.predict + estimate_confidence_score_mxif) on the
+//               staged row; label and confidence go to HBM, the blurred
+//               image never does
+// Every epilogue but kEpiStore takes its per-row side data (head slots or mask
+// bytes) through the raw DMA ring: each ring slot carries one more 1-KB DMA
+// piece past the raw input row, with the side data of the output row that the
+// same slot serves.
+template <typename T, int R, int CT, int BT, int EPI = kEpiStore>
 struct BlurMfmaCfg {
   static constexpr int NR = 2 * R + 1;
   static constexpr int BW = 16 * BT;            // output columns per band
@@ -112,48 +126,63 @@ struct BlurMfmaCfg {
   static constexpr int NW = NT / 64;
   static constexpr int ROW = NPX * PS;          // floats per LDS fp32 row buffer
   static constexpr int STG = BW * 16 * CT;      // floats per LDS output staging row (>= BW*C)
-  // raw input row segment: <= NPX * C elements, C <= 16*CT; NG 1-KB DMA pieces per wave
+  // raw input row segment: <= NPX * C elements, C <= 16*CT, fetched as NPC
+  // lane-linear 1-KB DMA pieces (piece i: wave i % NW, round i / NW); the
+  // fused epilogues add one piece for their per-row side data (index NPC)
   static constexpr int SEGMAX = NPX * 16 * CT * (int)sizeof(T);
-  static constexpr int NG = (SEGMAX + NW * 1024 - 1) / (NW * 1024);
-  static constexpr int SLOT = NG * NW * 1024;   // bytes per raw ring slot
-  static constexpr int NCH = SLOT / 16 / NT;    // 16-byte chunks per thread (= NG)
+  static constexpr int NPC = (SEGMAX + 1023) / 1024;
+  static constexpr int NPIECE = NPC + (EPI == kEpiStore ? 0 : 1);
+  static constexpr int NG = (NPIECE + NW - 1) / NW;  // DMA rounds (pieces of the busiest wave)
+  static constexpr int LASTW = NPIECE - (NG - 1) * NW;  // waves < LASTW issue NG pieces, the rest NG-1
+  static constexpr int SLOT = NPIECE * 1024;    // bytes per raw ring slot
+  static constexpr int NCH = (SLOT / 16 + NT - 1) / NT;  // 16-byte chunks per thread
   static constexpr int NP = NCH * Chunk16<T>::P;  // element pairs per thread
-  static constexpr size_t FIXED = (2 * (size_t)ROW + 2 * (size_t)STG) * sizeof(float) + 64;
-  // raw ring depth: 5 rows (4 in flight) when two workgroups then fit a CU's
-  // 160 KB of LDS, else as deep as one workgroup allows (<= 9); >= 4 (the
-  // launcher rejects configurations whose LDS does not fit)
+  static constexpr size_t EXTRA = EPI == kEpiAssign ? (size_t)8 * CT * kEpiKS * 8 : 0;  // centers
+  static constexpr size_t FIXED = (2 * (size_t)ROW + 2 * (size_t)STG) * sizeof(float) + 64 + EXTRA;
+  static constexpr int AUXOFF = NPC * 1024;     // side-data piece
+  static constexpr int AUXW = NPC % NW;
+  static constexpr int NS = NT / BW;            // epilogue threads per output column (4*CT)
+  // raw ring depth: as deep as two workgroups per CU allow (160 KB of LDS),
+  // up to DMAX rows (the DMA of row s+2 is waited for at step s: LA-2 steps
+  // of lead); one workgroup per CU only when two do not fit a 4-row ring
+#ifdef MW_BLUR_D
+  static constexpr int DMAX = MW_BLUR_D;
+#else
+  static constexpr int DMAX = 8;
+#endif
   static constexpr int D2 = ((80 * 1024 - (int)FIXED) / SLOT);
   static constexpr int D1 = ((160 * 1024 - (int)FIXED) / SLOT);
-#ifdef MW_BLUR_D
-  static constexpr int D = D1 >= MW_BLUR_D ? MW_BLUR_D : 4;
-#else
-  static constexpr int D = D2 >= 5 ? 5 : (D1 >= 9 ? 9 : (D1 >= 4 ? D1 : 4));
-#endif
+  static constexpr int D = D2 >= 4 ? (D2 < DMAX ? D2 : DMAX) : (D1 >= 4 ? (D1 < DMAX ? D1 : DMAX) : 4);
   static constexpr int LA = D - 1;              // rows in flight ahead of the converted one
   static constexpr size_t lds_bytes() { return FIXED + (size_t)D * SLOT; }
 };
 
-template <typename T, int R, int CT, int BT, bool LOGN>
-__global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __restrict__ in, int H, int W,
+template <typename T, int R, int CT, int BT, bool LOGN, int EPI>
+__global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_mfma_kernel(const T* __restrict__ in, int H, int W,
                                                                  int C, const float* __restrict__ inv_mean,
                                                                  float pseudo, BlurTaps taps,
-                                                                 float* __restrict__ out) {
-  using K = BlurMfmaCfg<T, R, CT, BT>;
+                                                                 float* __restrict__ out, BlurEpi ep) {
+  using K = BlurMfmaCfg<T, R, CT, BT, EPI>;
+  constexpr int NS = K::NS, KS = kEpiKS;
   constexpr int NR = K::NR, BW = K::BW, NPX = K::NPX, PS = K::PS, NK = K::NK, NT = K::NT;
   constexpr int ROW = K::ROW, STG = K::STG, NCH = K::NCH, NP = K::NP, CP = Chunk16<T>::P;
   constexpr int NG = K::NG, SLOT = K::SLOT, D = K::D, LA = K::LA;
   constexpr bool SWZ = K::SWZ;
   static_assert(LA >= 3, "raw ring too shallow");
-  // one step issues NG DMA pieces + 1 output store per wave; the DMA of row
-  // s+2 (issued at step s+2-LA) is followed by LA-2 steps' worth of them
-  constexpr int kWaitSteady = (LA - 2) * (NG + 1);
-  constexpr int kWaitEarly = (LA - 2) * NG + 1;  // steps s < LA-2 (prologue DMAs, no stores)
-  static_assert(kWaitSteady <= 63, "vmcnt field is 6 bits");
+  // one step issues NG (waves < LASTW) or NG-1 DMA pieces per wave + 1 output
+  // store (kEpiStore; the other epilogues issue only a data-dependent number
+  // of stores, which can only make a count stricter); the DMA of row s+2
+  // (issued at step s+2-LA) is followed by LA-2 steps' worth of them.  Waves
+  // without pieces wait for nothing.
+  constexpr int kStore = EPI == kEpiStore ? 1 : 0;
+  constexpr int NGB = NG - 1;  // pieces per step of waves >= LASTW
+  static_assert((LA - 2) * (NG + kStore) <= 63, "vmcnt field is 6 bits");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* s_rows = smem;                       // 2 x ROW  (fp32 input rows)
   float* s_stg = smem + 2 * ROW;              // 2 x STG  (output staging rows, HWC)
   float* s_dummy = smem + 2 * ROW + 2 * STG;  // 64 bytes: sink of pad pairs
   char* s_raw = reinterpret_cast<char*>(smem) + K::FIXED;  // D x SLOT raw input rows
+  f2m_* s_cT = reinterpret_cast<f2m_*>(s_dummy + 16);      // kEpiAssign: centers [pair][KS]
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -218,6 +247,33 @@ __global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __rest
   // check); thread t stores 16-byte chunk t, past the segment the range check drops it
   const uint32_t out_bytes = (uint32_t)bw * (uint32_t)C * 4u;
 
+  // ---- epilogue: thread (column ecol, part esub) of the staged output row
+  const int ecol = t / NS, esub = t % NS;
+  int fo[2][2];  // kEpiSample: channel of features 2*(esub + NS*i) + {0,1}, -1 past F
+  float sc_a = 1.f, sc_b = 0.f;  // kEpiAssign: scaler of this lane's vertical-pass channel
+  uint32_t aux_off = 0;
+  if constexpr (EPI == kEpiSample) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int f0 = 2 * (esub + NS * i);
+      fo[i][0] = f0 < ep.F ? ep.feat[f0] : -1;
+      fo[i][1] = f0 + 1 < ep.F ? ep.feat[f0 + 1] : -1;
+    }
+    aux_off = (uint32_t)lane * 16u < (uint32_t)(BW + 4) * 4u ? (uint32_t)lane * 16u : 0u;
+  }
+  if constexpr (EPI == kEpiAssign) {
+    for (int q = t; q < 8 * CT * KS; q += NT) {
+      const int p = q / KS, j = q - p * KS;
+      const bool ok = j < ep.k && 2 * p < C;  // C even (launcher)
+      s_cT[q] = ok ? f2m_{ep.centers[j * C + 2 * p], ep.centers[j * C + 2 * p + 1]} : f2m_{0.f, 0.f};
+    }
+    if (st_ok) {
+      sc_a = ep.a[16 * ct + m];
+      sc_b = ep.b[16 * ct + m];
+    }
+    aux_off = (uint32_t)lane * 16u < (uint32_t)(BW + 16) ? (uint32_t)lane * 16u : 0u;
+  }
+
   f4m ring[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) ring[j] = f4m{0.f, 0.f, 0.f, 0.f};
@@ -229,14 +285,38 @@ __global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __rest
     const char* src = reinterpret_cast<const char*>(in + ((int64_t)yy * W + xa) * C);
     const uint32_t slot = raw0 + (uint32_t)(q % D) * SLOT;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) glds16(src, g_off[g], slot + (uint32_t)(g * NT + 64 * wv) * 16u);
+    for (int g = 0; g < NG; ++g) {
+      if (g == NG - 1 && wv >= K::LASTW) continue;  // piece past the slot
+      if constexpr (EPI != kEpiStore) {
+        if (g == NG - 1 && wv == K::AUXW) {
+          // side data of output row y0 + q - 2 - 2R (the row stored at step q),
+          // from the 16-byte aligned address at or below its first pixel
+          int yq = y0 + q - 2 - 2 * R;
+          yq = yq < y0 ? y0 : (yq >= y1 ? y1 - 1 : yq);
+          const int64_t rp = (int64_t)yq * W + x0;
+          const char* asrc = EPI == kEpiSample
+                                 ? reinterpret_cast<const char*>(ep.head) + ((rp * 4) & ~(int64_t)15)
+                                 : reinterpret_cast<const char*>(ep.mask) + (rp & ~(int64_t)15);
+          glds16(asrc, aux_off, slot + (uint32_t)(g * NT + 64 * wv) * 16u);
+          continue;
+        }
+      }
+      glds16(src, g_off[g], slot + (uint32_t)(g * NT + 64 * wv) * 16u);
+    }
   };
   auto convert_row = [&](int q) {
     float* dst = s_rows + (q & 1) * ROW;
     const char* raw = s_raw + (q % D) * SLOT;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const u4m v = *reinterpret_cast<const u4m*>(raw + (t + c * NT) * 16);
+      // waves whose chunks are all past the segment skip the conversion (pad
+      // pairs only; wave-uniform branch): with BW*C small enough that the
+      // segment fits four waves, every SIMD converts one chunk per row
+      if ((uint32_t)(64 * wv + c * NT) * 16u >= seg_bytes) continue;
+      // chunks past the slot (SLOT is not a multiple of NT*16) are pad pairs
+      const u4m v = (c + 1) * NT * 16 <= SLOT || (t + c * NT) * 16 < SLOT
+                        ? *reinterpret_cast<const u4m*>(raw + (t + c * NT) * 16)
+                        : u4m{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int i = 0; i < CP; ++i) {
         bf2 x = Chunk16<T>::pair(v, i);
@@ -271,13 +351,83 @@ __global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __rest
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4m, v), ro, t * 16, 0, 0);
   };
 
+  // kEpiSample / kEpiAssign on the output row staged at step s-1 (buffer s & 1)
+  auto epilogue = [&](int s) {
+    asm volatile("" : "+s"(s));  // per-step values stay per step (no hoisting across the unroll)
+    const int yo = y0 + s - 2 - 2 * R;
+    const int64_t rowpix = (int64_t)yo * W + x0;
+    const char* auxp = s_raw + (s % D) * SLOT + K::AUXOFF;
+    const float* srow = s_stg + (s & 1) * STG + ecol * C;
+    if constexpr (EPI == kEpiSample) {
+      const int h = reinterpret_cast<const int*>(auxp)[(int)(rowpix & 3) + ecol];
+      if (ecol < bw && (uint64_t)(uint32_t)h < (uint64_t)ep.S) {
+        float* dst = ep.X + (int64_t)h * ep.F;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int f0 = 2 * (esub + NS * i);
+          if (fo[i][0] < 0) continue;
+          const float v0 = srow[fo[i][0]];
+          if (fo[i][1] >= 0 && (ep.F & 1) == 0) {
+            *reinterpret_cast<f2m_*>(dst + f0) = f2m_{v0, srow[fo[i][1]]};
+          } else {
+            dst[f0] = v0;
+            if (fo[i][1] >= 0) dst[f0 + 1] = srow[fo[i][1]];
+          }
+        }
+      }
+    } else {
+      // distances of this column's pixel to centers esub and esub + NS: the
+      // Lloyd/assign E-step chain (even features in .x, odd in .y, pair order)
+      const uint8_t mk = reinterpret_cast<const uint8_t*>(auxp)[(int)(rowpix & 15) + ecol];
+      const f2m_* xp = reinterpret_cast<const f2m_*>(srow);
+      const f2m_* cp = s_cT + esub;
+      const int np = C >> 1;
+      f2m_ acc0 = f2m_{0.f, 0.f}, acc1 = f2m_{0.f, 0.f};
+      if (ep.k > NS) {
+        for (int p = 0; p < np; ++p) {
+          const f2m_ x = xp[p];
+          const f2m_ d0 = x - cp[p * KS], d1 = x - cp[p * KS + NS];
+          acc0 = __builtin_elementwise_fma(d0, d0, acc0);
+          acc1 = __builtin_elementwise_fma(d1, d1, acc1);
+        }
+      } else {
+        for (int p = 0; p < np; ++p) {
+          const f2m_ d0 = xp[p] - cp[p * KS];
+          acc0 = __builtin_elementwise_fma(d0, d0, acc0);
+        }
+      }
+      const float dd0 = acc0.x + acc0.y, dd1 = acc1.x + acc1.y;
+      // strict argmin in center order + second smallest (nearest_centers<TOP2>)
+      const int lb = lane & ~(NS - 1);
+      int lab = 0;
+      float m1 = 0.f, m2 = __builtin_inff();
+      for (int j = 0; j < ep.k; ++j) {
+        const float dd = __shfl(j < NS ? dd0 : dd1, lb + (j & (NS - 1)), 64);
+        if (j == 0) { m1 = dd; lab = 0; }
+        else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
+        else if (dd < m2) { m2 = dd; }
+      }
+      const bool in_mask = ecol < bw && mk != 0;
+      const float conf = in_mask ? (m2 - m1) / m2 : __builtin_nanf("");
+      if (!in_mask) lab = -1;
+      if (esub == 0 && ecol < bw) {
+        ep.lab[rowpix + ecol] = (int8_t)lab;
+        ep.conf[rowpix + ecol] = conf;
+      }
+    }
+  };
+
   lds_barrier();  // zero fill done
 #pragma unroll
   for (int q = 0; q < LA; ++q) dma_row(q);
-  vm_wait_n<(LA - 1) * NG>();  // row 0 landed (this wave's pieces)
+  // the wait counts of this wave (full: NG pieces per row, else NG-1)
+  const bool full = wv < K::LASTW;
+  if (full) vm_wait_n<(LA - 1) * NG>();  // row 0 landed (this wave's pieces)
+  else if (NGB > 0) vm_wait_n<(LA - 1) * (NGB > 0 ? NGB : 1)>();
   lds_barrier();
   convert_row(0);
-  vm_wait_n<(LA - 2) * NG>();  // row 1 landed
+  if (full) vm_wait_n<(LA - 2) * NG>();  // row 1 landed
+  else if (NGB > 0) vm_wait_n<(LA - 2) * (NGB > 0 ? NGB : 1)>();
   lds_barrier();
   // step s: convert input row s+1, MFMA row s, vertical pass of row s-1 into
   // staging, store the output row staged at step s-1, DMA of row s+LA; wait
@@ -309,7 +459,11 @@ __global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __rest
           u0 = __builtin_elementwise_fma(w2, bf2{rg.z, rg.w}, u0);
         }
       }
-      const bf2 va = v0 + v1, vb = u0 + u1;
+      bf2 va = v0 + v1, vb = u0 + u1;
+      if constexpr (EPI == kEpiAssign) {  // StandardScaler: x * a + b (the assign kernel's fma)
+        va = __builtin_elementwise_fma(va, bf2{sc_a, sc_a}, bf2{sc_b, sc_b});
+        vb = __builtin_elementwise_fma(vb, bf2{sc_a, sc_a}, bf2{sc_b, sc_b});
+      }
       if (st_ok) {
         float* sg = s_stg + ((s - 1) & 1) * STG + st_base;
         sg[0] = va.x;
@@ -318,7 +472,15 @@ __global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __rest
         sg[3 * C] = vb.y;
       }
     }
-    store_out(s & 1, y0 + s - 2 - 2 * R, !guard || s >= 2 + 2 * R);
+    if constexpr (EPI == kEpiStore) {
+      store_out(s & 1, y0 + s - 2 - 2 * R, !guard || s >= 2 + 2 * R);
+    } else if (!guard || s >= 2 + 2 * R) {
+      // kept apart from the other stages: interleaved, the epilogue's
+      // temporaries would lift the kernel past 128 VGPRs (one workgroup per CU)
+      __builtin_amdgcn_sched_barrier(0);
+      epilogue(s);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     dma_row(s + LA);
     if (!guard || s < nrows) {
       f4m d0 = f4m{0.f, 0.f, 0.f, 0.f}, d1 = f4m{0.f, 0.f, 0.f, 0.f};
@@ -329,8 +491,13 @@ __global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __rest
       }
       ring[j] = d0 + d1;
     }
-    if (guard && s < LA - 2) vm_wait_n<kWaitEarly>();
-    else vm_wait_n<kWaitSteady>();
+    if (full) {
+      if (guard && s < LA - 2) vm_wait_n<(LA - 2) * NG + kStore>();  // prologue DMAs, no stores yet
+      else vm_wait_n<(LA - 2) * (NG + kStore)>();
+    } else if (NGB > 0) {
+      if (guard && s < LA - 2) vm_wait_n<(LA - 2) * (NGB > 0 ? NGB : 1) + kStore>();
+      else vm_wait_n<(LA - 2) * ((NGB > 0 ? NGB : 1) + kStore)>();
+    }
     lds_barrier();
   };
   // steady groups: NR-aligned, all of s in [2R+2, nrows-2], interior bands
@@ -355,33 +522,41 @@ __global__ void __launch_bounds__(64 * BT * CT) blur_mfma_kernel(const T* __rest
   vm_wait_n<0>();  // no DMA may still target this workgroup's LDS at exit
 }
 
-template <typename T, int R, int CT, int BT>
+template <typename T, int R, int CT, int BT, int EPI>
 static int launch_blur_mfma_rc(const T* in, int H, int W, int C, const float* inv_mean, float p,
-                               const BlurTaps& taps, float* out, hipStream_t st) {
-  using K = BlurMfmaCfg<T, R, CT, BT>;
-  const size_t lds = K::lds_bytes();
-  if (lds > 160 * 1024 || K::D < 4) return MW_EUNSUPPORTED;
-  dim3 grid((W + K::BW - 1) / K::BW, (H + kBlurBH - 1) / kBlurBH);
-  if (inv_mean)
-    hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, true>), grid, dim3(K::NT), lds, st, in, H, W,
-                       C, inv_mean, p, taps, out);
-  else
-    hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, false>), grid, dim3(K::NT), lds, st, in, H, W,
-                       C, inv_mean, p, taps, out);
-  MW_LAUNCH_CHECK();
-  return MW_OK;
+                               const BlurTaps& taps, float* out, const BlurEpi& ep, hipStream_t st) {
+  using K = BlurMfmaCfg<T, R, CT, BT, EPI>;
+  {
+    const size_t lds = K::lds_bytes();
+    if (lds > 160 * 1024 || K::D < 4) return MW_EUNSUPPORTED;
+    dim3 grid((W + K::BW - 1) / K::BW, (H + kBlurBH - 1) / kBlurBH);
+    if (inv_mean) {
+      hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, true, EPI>), grid, dim3(K::NT), lds, st, in, H,
+                         W, C, inv_mean, p, taps, out, ep);
+    } else if constexpr (EPI == kEpiStore) {
+      hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, false, EPI>), grid, dim3(K::NT), lds, st, in, H,
+                         W, C, inv_mean, p, taps, out, ep);
+    } else {
+      return MW_EUNSUPPORTED;  // the fused epilogues follow a log-normalise
+    }
+    MW_LAUNCH_CHECK();
+    return MW_OK;
+  }
 }
 
 template <typename T, int R>
 static int launch_blur_mfma_r(const T* in, int H, int W, int C, const float* inv_mean, float p,
                               const BlurTaps& taps, float* out, hipStream_t st) {
-  static const int bt = [] {  // column tiles per band (tuning override MW_BLUR_BT = 2 or 4)
+  static const int bt = [] {  // column tiles per band (tuning override MW_BLUR_BT = 2, 3 or 4)
     const char* e = getenv("MW_BLUR_BT");
-    return (e && atoi(e) == 2) ? 2 : 4;
+    const int v = e ? atoi(e) : 4;
+    return (v == 2 || v == 3) ? v : 4;
   }();
-#define MW_BT(CTV)                                                                            \
-  return bt == 4 ? launch_blur_mfma_rc<T, R, CTV, 4>(in, H, W, C, inv_mean, p, taps, out, st) \
-                 : launch_blur_mfma_rc<T, R, CTV, 2>(in, H, W, C, inv_mean, p, taps, out, st);
+  const BlurEpi ep{};
+#define MW_BT(CTV)                                                                                 \
+  return bt == 4 ? launch_blur_mfma_rc<T, R, CTV, 4, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st) \
+       : bt == 3 ? launch_blur_mfma_rc<T, R, CTV, 3, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st) \
+                 : launch_blur_mfma_rc<T, R, CTV, 2, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
   if (C <= 16) { MW_BT(1) }
   if (C <= 32) { MW_BT(2) }
   if (C <= 48) { MW_BT(3) }
@@ -389,22 +564,72 @@ static int launch_blur_mfma_r(const T* in, int H, int W, int C, const float* inv
 #undef MW_BT
 }
 
+// fused epilogue launch (BT = 4); the per-epilogue limits depend on CT
+template <typename T, int R, int CT>
+static int launch_blur_epi_rc(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                              const BlurTaps& taps, const BlurEpi& ep, int epi, hipStream_t st) {
+  constexpr int NS = BlurMfmaCfg<T, R, CT, 4>::NS;
+  if (epi == kEpiSample) {
+    if (ep.F > 16 * CT) return MW_EUNSUPPORTED;
+    return launch_blur_mfma_rc<T, R, CT, 4, kEpiSample>(in, H, W, C, inv_mean, p, taps, nullptr, ep, st);
+  }
+  if (ep.k > 2 * NS || ep.k > kEpiKS) return MW_EUNSUPPORTED;
+  return launch_blur_mfma_rc<T, R, CT, 4, kEpiAssign>(in, H, W, C, inv_mean, p, taps, nullptr, ep, st);
+}
+template <typename T, int R>
+static int launch_blur_epi_r(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                             const BlurTaps& taps, const BlurEpi& ep, int epi, hipStream_t st) {
+  if (C <= 16) return launch_blur_epi_rc<T, R, 1>(in, H, W, C, inv_mean, p, taps, ep, epi, st);
+  if (C <= 32) return launch_blur_epi_rc<T, R, 2>(in, H, W, C, inv_mean, p, taps, ep, epi, st);
+  if (C <= 48) return launch_blur_epi_rc<T, R, 3>(in, H, W, C, inv_mean, p, taps, ep, epi, st);
+  return launch_blur_epi_rc<T, R, 4>(in, H, W, C, inv_mean, p, taps, ep, epi, st);
+}
+
+// the shape limits of the matrix-core kernel (all epilogues)
+static inline bool blur_mfma_shape_ok(int W, int C, int r, size_t elem) {
+  if (C % 2 != 0 || C > 64 || r < 1 || r > kBlurMfmaMaxR) return false;
+  // 16-byte output chunks: every band's row segment is a whole number of them
+  if (((int64_t)W * C) % 4 != 0) return false;
+  // 16-byte DMA pieces read whole dwords of the input rows
+  if (((int64_t)W * C * (int64_t)elem) % 4 != 0) return false;
+  return (int64_t)W * C * 4 < 0x7FFFFFF0ll;
+}
+
+// Fused blur + kEpiSample / kEpiAssign epilogue; MW_EUNSUPPORTED when the
+// shape or the epilogue limits rule it out (the caller then materialises the
+// blurred image and runs the standalone gather / assign kernels).
+template <typename T>
+int launch_blur_epi(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                    const BlurTaps& taps, int r, const BlurEpi& ep, int epi, hipStream_t st) {
+  if (!blur_mfma_shape_ok(W, C, r, sizeof(T)) || inv_mean == nullptr) return MW_EUNSUPPORTED;
+  if (epi != kEpiSample && epi != kEpiAssign) return MW_EUNSUPPORTED;
+  switch (r) {
+#define MW_R(N) case N: return launch_blur_epi_r<T, N>(in, H, W, C, inv_mean, p, taps, ep, epi, st);
+#ifdef MW_BLUR_DEV  // development builds: radius 8 only (sigma 2)
+    MW_R(8)
+#else
+    MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8)
+#endif
+#undef MW_R
+    default: return MW_EUNSUPPORTED;
+  }
+}
+
 // MFMA path for even C <= 64, 1 <= r <= 8, rows that fit 32-bit offsets;
 // MW_EUNSUPPORTED otherwise (the caller tries the next path).
 template <typename T>
 int launch_blur_mfma(const T* in, int H, int W, int C, const float* inv_mean, float p,
                      const BlurTaps& taps, int r, float* out, hipStream_t st) {
-  if (C % 2 != 0 || C > 64 || r < 1 || r > kBlurMfmaMaxR) return MW_EUNSUPPORTED;
-  // 16-byte output chunks: every band's row segment is a whole number of them
-  if (((int64_t)W * C) % 4 != 0) return MW_EUNSUPPORTED;
-  // 16-byte DMA pieces read whole dwords of the input rows
-  if (((int64_t)W * C * (int64_t)sizeof(T)) % 4 != 0) return MW_EUNSUPPORTED;
-  if ((int64_t)W * C * 4 >= 0x7FFFFFF0ll) return MW_EUNSUPPORTED;
+  if (!blur_mfma_shape_ok(W, C, r, sizeof(T))) return MW_EUNSUPPORTED;
   if (const char* e = getenv("MW_BLUR_IMPL"))
     if (e[0] == 'v') return MW_EUNSUPPORTED;  // force the VALU kernel (A/B tests)
   switch (r) {
 #define MW_R(N) case N: return launch_blur_mfma_r<T, N>(in, H, W, C, inv_mean, p, taps, out, st);
+#ifdef MW_BLUR_DEV
+    MW_R(8)
+#else
     MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8)
+#endif
 #undef MW_R
     default: return MW_EUNSUPPORTED;
   }

@@ -1,0 +1,8 @@
+// Fused blur + subsample / label epilogue instances for uint8_t input (blur_mfma.h):
+// a translation unit of their own so the blur kernels build in parallel.
+#include "blur_mfma.h"
+
+namespace mw {
+template int launch_blur_epi<uint8_t>(const uint8_t*, int, int, int, const float*, float, const BlurTaps&, int,
+                                   const BlurEpi&, int, hipStream_t);
+}  // namespace mw

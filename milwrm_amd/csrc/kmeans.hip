@@ -949,6 +949,65 @@ __global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float*
   }
 }
 
+// Per-block domain records [sum conf k | count k] from label/confidence maps
+// (the fused blur assign epilogue writes only the maps): the assign kernel's
+// block partition, wave/tile order and lane-private fp64 slots, so the
+// records, and the domain means, are the same numbers it produces.
+__global__ void __launch_bounds__(256) domain_records_kernel(const int8_t* __restrict__ lab,
+                                                             const float* __restrict__ conf, int k,
+                                                             int64_t n, int64_t R,
+                                                             double* __restrict__ rec) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
+  const size_t wslot = (size_t)(k + 1) * 64 * 12;
+  char* wb = smem + (size_t)wid * wslot;
+  double* w_csum = reinterpret_cast<double*>(wb);
+  unsigned* w_ccnt = reinterpret_cast<unsigned*>(w_csum + (k + 1) * 64);
+  for (int q = lane; q < (k + 1) * 64; q += 64) {
+    w_csum[q] = 0.0;
+    w_ccnt[q] = 0u;
+  }
+  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(n, lo + R);
+  const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
+  for (int tc = wid; tc < ntile; tc += nw) {
+    const int64_t p = lo + (int64_t)tc * 64 + lane;
+    const bool valid = p < hi;
+    const int lb = valid ? (int)lab[p] : -1;
+    const float c = valid ? conf[p] : 0.f;
+    const int slot = (lb < 0 ? k : lb) * 64 + lane;
+    w_csum[slot] += lb >= 0 ? (double)c : 0.0;
+    w_ccnt[slot] += 1u;
+  }
+  __syncthreads();
+  double* out = rec + (size_t)blockIdx.x * 2 * k;
+  for (int q = t; q < 2 * k; q += blockDim.x) {
+    const int j = q < k ? q : q - k;
+    double sacc = 0.0;
+    for (int w = 0; w < nw; ++w) {
+      const double* cs = reinterpret_cast<const double*>(smem + (size_t)w * wslot);
+      const unsigned* cc = reinterpret_cast<const unsigned*>(cs + (k + 1) * 64);
+      if (q < k) {
+        for (int l = 0; l < 64; ++l) sacc += cs[j * 64 + l];
+      } else {
+        unsigned long long cn = 0;
+        for (int l = 0; l < 64; ++l) cn += cc[j * 64 + l];
+        sacc += (double)cn;
+      }
+    }
+    out[q] = sacc;
+  }
+}
+
+// waves per assign block (LDS-bound for large k and C): shared with the
+// domain-records kernel so both partition the image the same way
+static int assign_waves(int k, int C) {
+  const int CM = C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64;
+  const size_t cent = cent_t_bytes(k <= 64 ? 64 : 128, CM);
+  int nw = 4;
+  while (nw > 1 && cent + nw * assign_wave_bytes(k, CM) > 160 * 1024) --nw;
+  return nw;
+}
+
 }  // namespace mw
 
 using namespace mw;
@@ -1192,8 +1251,7 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
 #define MW_AS(CM, KSV)                                                                          \
   {                                                                                             \
     const size_t cent = cent_t_bytes(KSV, CM);                                                  \
-    int nw = 4;                                                                                 \
-    while (nw > 1 && cent + nw * assign_wave_bytes(k, CM) > 160 * 1024) --nw;                   \
+    const int nw = assign_waves(k, C);                                                          \
     const size_t lds = cent + nw * assign_wave_bytes(k, CM);                                    \
     if (lds > 160 * 1024) {                                                                     \
       set_error("mw_assign_conf: LDS %zu too large (C=%d k=%d)", lds, C, k);                    \
@@ -1211,6 +1269,22 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
   else { MW_ASK(64) }
 #undef MW_ASK
 #undef MW_AS
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_domain_records(const int8_t* d_label, const float* d_conf, int64_t n_pix, int C, int k,
+                      void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_label && d_conf && d_ws && n_pix > 0 && C > 0 && k >= 1 && k <= 127,
+               "mw_domain_records: bad args");
+  const int nw = assign_waves(k, C);
+  const size_t lds = (size_t)nw * (k + 1) * 64 * 12;
+  if (lds > 160 * 1024) {
+    set_error("mw_domain_records: k=%d too large", k);
+    return MW_EUNSUPPORTED;
+  }
+  hipLaunchKernelGGL(domain_records_kernel, dim3(kblocks(n_pix)), dim3(64 * nw), lds, as_stream(stream),
+                     d_label, d_conf, k, n_pix, krows(n_pix), reinterpret_cast<double*>(d_ws));
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

@@ -376,6 +376,10 @@ __device__ __forceinline__ void chan_merge(double& n_a, double& m_a, double& q_a
   n_a = n;
 }
 
+// GATHER false: the rows are already in X (written by the fused blur sample
+// epilogue) and only the statistics are taken, over the same block/tile
+// partition and in the same order, so both give identical records.
+template <bool GATHER>
 __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ img, int C,
                                                      const int32_t* __restrict__ feat, int F,
                                                      const int32_t* __restrict__ idx,
@@ -386,7 +390,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   __shared__ int s_feat[64];
   __shared__ uint32_t s_pix[256];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  for (int f = t; f < 64; f += 256) s_feat[f] = f < F ? feat[f] : 0;
+  for (int f = t; f < 64; f += 256) s_feat[f] = (GATHER && f < F) ? feat[f] : 0;
   const int nparts = 256 / F;
   const bool st_on = t < nparts * F;
   const int sf = st_on ? t % F : 0, spart = st_on ? t / F : 0;
@@ -398,10 +402,10 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   const int64_t lo = (int64_t)blockIdx.x * R;
   const int64_t hi = min(S, lo + R);
   __syncthreads();
-  const int fcol = lf < F ? s_feat[lf] : 0;
+  const int fcol = lf < F ? (GATHER ? s_feat[lf] : lf) : 0;
   for (int64_t r0 = lo; r0 < hi; r0 += kTile) {
     const int nrow = (int)min((int64_t)kTile, hi - r0);
-    if (t < nrow) s_pix[t] = r2p[idx[r0 + t]];
+    if (GATHER && t < nrow) s_pix[t] = r2p[idx[r0 + t]];
     __syncthreads();
     // wave wid loads rows [wid*64, wid*64+64) of the tile, RPI rows per instruction
     constexpr int kBatch = 16;
@@ -410,7 +414,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
 #pragma unroll
       for (int i = 0; i < kBatch; ++i) {
         const int row = min(wid * 64 + (i0 + i) * RPI + lr, nrow - 1);  // clamped: always valid
-        v[i] = img[(int64_t)s_pix[row] * C + fcol];
+        v[i] = GATHER ? img[(int64_t)s_pix[row] * C + fcol] : X[(r0 + row) * F + fcol];
       }
 #pragma unroll
       for (int i = 0; i < kBatch; ++i) {
@@ -420,9 +424,11 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
     }
     __syncthreads();
     // coalesced write of the tile (rows contiguous in X)
-    float* dst = X + r0 * F;
-    const int ne = nrow * F;
-    for (int q = t; q < ne; q += 256) dst[q] = s_tile[q];
+    if (GATHER) {
+      float* dst = X + r0 * F;
+      const int ne = nrow * F;
+      for (int q = t; q < ne; q += 256) dst[q] = s_tile[q];
+    }
     // column statistics of this tile part
     if (st_on) {
       double s = 0.0, cnt = 0.0;
@@ -700,10 +706,140 @@ int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F, cons
   const int64_t R = rows_per_block(S);
   size_t lds = (size_t)kTile * F * sizeof(float);
   if (lds < 3 * 256 * sizeof(double)) lds = 3 * 256 * sizeof(double);
-  hipLaunchKernelGGL(gather_kernel, dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_idx,
+  hipLaunchKernelGGL(gather_kernel<true>, dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_idx,
                      d_rank2pix, S, R, d_X, reinterpret_cast<double*>(d_ws));
   MW_LAUNCH_CHECK();
   return MW_OK;
+}
+
+int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_X && d_ws, "mw_col_stats_rows: null pointer");
+  MW_CHECK_ARG(S > 0 && F > 0 && F <= 64, "mw_col_stats_rows: bad shape S=%lld F=%d", (long long)S, F);
+  hipStream_t st = as_stream(stream);
+  size_t lds = (size_t)kTile * F * sizeof(float);
+  if (lds < 3 * 256 * sizeof(double)) lds = 3 * 256 * sizeof(double);
+  hipLaunchKernelGGL(gather_kernel<false>, dim3(stream_blocks(S)), dim3(256), lds, st, nullptr, F,
+                     nullptr, F, nullptr, nullptr, S, rows_per_block(S), const_cast<float*>(d_X),
+                     reinterpret_cast<double*>(d_ws));
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+// ------------------------------------------------- fused blur + subsample
+// head[p] = smallest sample slot j with rank2pix[idx[j]] == p (int32 max: p
+// not sampled), pix[j] = that pixel.  The blur's sample epilogue writes row
+// head[p] of X; sample_fixup copies it to the other slots of p (idx draws
+// with replacement).
+__global__ void __launch_bounds__(256) sample_map_kernel(const int32_t* __restrict__ idx,
+                                                         const uint32_t* __restrict__ r2p, int64_t S,
+                                                         int32_t* __restrict__ head,
+                                                         int32_t* __restrict__ pix) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < S; j += (int64_t)gridDim.x * 256) {
+    const uint32_t p = r2p[idx[j]];
+    pix[j] = (int32_t)p;
+    atomicMin(head + p, (int32_t)j);
+  }
+}
+__global__ void __launch_bounds__(256) sample_fixup_kernel(const int32_t* __restrict__ pix,
+                                                           const int32_t* __restrict__ head, int64_t S,
+                                                           int F, float* __restrict__ X) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < S; j += (int64_t)gridDim.x * 256) {
+    const int32_t h = head[pix[j]];
+    if (h != (int32_t)j) {
+      const float* src = X + (int64_t)h * F;
+      float* dst = X + j * F;
+      for (int f = 0; f < F; ++f) dst[f] = src[f];
+    }
+  }
+}
+
+size_t mw_sample_head_elems(int64_t n_pix) { return (size_t)n_pix + 128; }
+
+int mw_sample_map(const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S, int64_t n_pix,
+                  int32_t* d_head, int32_t* d_pix, void* stream) {
+  MW_CHECK_ARG(d_idx && d_rank2pix && d_head && d_pix, "mw_sample_map: null pointer");
+  MW_CHECK_ARG(S > 0 && S < 0x7fffffffll && n_pix > 0, "mw_sample_map: bad sizes S=%lld n_pix=%lld",
+               (long long)S, (long long)n_pix);
+  hipStream_t st = as_stream(stream);
+  MW_HIP(hipMemsetAsync(d_head, 0x7f, mw_sample_head_elems(n_pix) * sizeof(int32_t), st));
+  const int grid = (int)std::min<int64_t>((S + 255) / 256, 8192);
+  hipLaunchKernelGGL(sample_map_kernel, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, S, d_head, d_pix);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_sample_fixup(const int32_t* d_pix, const int32_t* d_head, int64_t S, int F, float* d_X,
+                    void* stream) {
+  MW_CHECK_ARG(d_pix && d_head && d_X && S > 0 && F > 0, "mw_sample_fixup: bad args");
+  hipStream_t st = as_stream(stream);
+  const int grid = (int)std::min<int64_t>((S + 255) / 256, 8192);
+  hipLaunchKernelGGL(sample_fixup_kernel, dim3(grid), dim3(256), 0, st, d_pix, d_head, S, F, d_X);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+static int blur_taps_from_host(const float* h_w, int radius, BlurTaps& taps) {
+  if (radius < 0 || radius > kMaxRadius) return MW_EUNSUPPORTED;
+  memset(&taps, 0, sizeof(taps));
+  for (int j = 0; j <= 2 * radius; ++j) taps.w[j] = h_w[j];
+  return MW_OK;
+}
+
+static int blur_epi_dispatch(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
+                             float pseudoval, const float* h_w, int radius, const BlurEpi& ep, int epi,
+                             void* stream, const char* who) {
+  BlurTaps taps;
+  if (blur_taps_from_host(h_w, radius, taps) != MW_OK) {
+    set_error("%s: radius %d unsupported", who, radius);
+    return MW_EUNSUPPORTED;
+  }
+  hipStream_t st = as_stream(stream);
+  int rc;
+  switch (dtype) {
+    case MW_U8: rc = launch_blur_epi<uint8_t>((const uint8_t*)d_img, H, W, C, d_inv_mean, pseudoval, taps, radius, ep, epi, st); break;
+    case MW_U16: rc = launch_blur_epi<uint16_t>((const uint16_t*)d_img, H, W, C, d_inv_mean, pseudoval, taps, radius, ep, epi, st); break;
+    case MW_F32: rc = launch_blur_epi<float>((const float*)d_img, H, W, C, d_inv_mean, pseudoval, taps, radius, ep, epi, st); break;
+    default: set_error("%s: bad dtype %d", who, dtype); return MW_EINVAL;
+  }
+  if (rc == MW_EUNSUPPORTED)
+    set_error("%s: no fused kernel for dtype %d C=%d W=%d radius %d (materialise the blur instead)", who,
+              dtype, C, W, radius);
+  return rc;
+}
+
+int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
+                   float pseudoval, const float* h_w, int radius, const int32_t* d_head, int64_t S,
+                   const int32_t* d_feat, int F, float* d_X, void* stream) {
+  MW_CHECK_ARG(d_img && d_inv_mean && h_w && d_head && d_feat && d_X, "mw_blur_sample: null pointer");
+  MW_CHECK_ARG(H > 0 && W > 0 && C > 0 && F > 0 && S > 0 && S < 0x7fffffffll,
+               "mw_blur_sample: bad shape");
+  BlurEpi ep{};
+  ep.head = d_head;
+  ep.S = S;
+  ep.X = d_X;
+  ep.F = F;
+  ep.feat = d_feat;
+  return blur_epi_dispatch(d_img, dtype, H, W, C, d_inv_mean, pseudoval, h_w, radius, ep, kEpiSample,
+                           stream, "mw_blur_sample");
+}
+
+int mw_blur_assign_conf(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
+                        float pseudoval, const float* h_w, int radius, const float* d_a,
+                        const float* d_b, const float* d_centers, int k, const uint8_t* d_mask,
+                        int8_t* d_label, float* d_conf, void* stream) {
+  MW_CHECK_ARG(d_img && d_inv_mean && h_w && d_a && d_b && d_centers && d_mask && d_label && d_conf,
+               "mw_blur_assign_conf: null pointer");
+  MW_CHECK_ARG(H > 0 && W > 0 && C > 0 && k >= 1, "mw_blur_assign_conf: bad shape");
+  BlurEpi ep{};
+  ep.mask = d_mask;
+  ep.lab = d_label;
+  ep.conf = d_conf;
+  ep.a = d_a;
+  ep.b = d_b;
+  ep.centers = d_centers;
+  ep.k = k;
+  return blur_epi_dispatch(d_img, dtype, H, W, C, d_inv_mean, pseudoval, h_w, radius, ep, kEpiAssign,
+                           stream, "mw_blur_assign_conf");
 }
 
 int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats, int accumulate,

@@ -3,6 +3,8 @@
 every computation is a hand-written HIP kernel in ``csrc/``)."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -186,6 +188,77 @@ def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2
         N.call("mw_gather_rows", P(img_f32), C, P(feat), F, P(idx), P(r2p), S, P(X_out), P(ws),
                stream())
     N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
+
+
+def col_stats_rows(X: torch.Tensor, stats: torch.Tensor, accumulate: bool):
+    """Column statistics of rows already in ``X`` (the records mw_gather_rows
+    would produce for the same rows), Chan-merged into ``stats``."""
+    S, F = X.shape
+    if S == 0:
+        return
+    ws = WS.get("gather", N.query("mw_gather_ws_bytes", S, F))
+    with profiling.timed("col_stats", S * F * 4):
+        N.call("mw_col_stats_rows", P(X), S, F, P(ws), stream())
+    N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
+
+
+FUSED_USED = {"sample": 0, "assign": 0}  # fused-epilogue launches taken (tests read it)
+
+
+def defer_blur(H: int, W: int, C: int) -> bool:
+    """Whether ``img.blurring`` defers the Gaussian into the fused epilogues
+    (subsample gather and label pass recompute it from the raw slide, the
+    fp32 blurred slide is never stored).  ``MW_FUSED_BLUR`` = 1 / 0 forces
+    it; by default ("auto") only when the fp32 slide would take more than
+    half of the free HBM -- at config 2 materialising is faster (the label
+    pass then reads 4 bytes per element instead of recomputing 17x17 taps)."""
+    mode = os.environ.get("MW_FUSED_BLUR", "auto")
+    if mode in ("0", "1"):
+        return mode == "1"
+    free, _ = torch.cuda.mem_get_info()
+    return H * W * C * 4 > free // 2
+
+
+def padded_mask(mask_u8: torch.Tensor, pad: int = 256) -> torch.Tensor:
+    """``mask_u8`` in a buffer readable ``pad`` bytes past its end (the fused
+    assign epilogue DMAs whole 1-KB pieces of mask rows)."""
+    n = mask_u8.numel()
+    st = mask_u8.untyped_storage()
+    if mask_u8.is_contiguous() and st.nbytes() - mask_u8.storage_offset() >= n + pad:
+        return mask_u8
+    buf = torch.zeros(n + pad, dtype=torch.uint8, device=mask_u8.device)
+    buf[:n].copy_(mask_u8.reshape(-1))
+    return buf[:n].view(mask_u8.shape)
+
+
+def blur_gather_fused(img: torch.Tensor, sigma: float, inv_mean, pseudoval: float,
+                      feat: torch.Tensor, idx: torch.Tensor, r2p: torch.Tensor, X_out: torch.Tensor,
+                      truncate: float = 4.0) -> bool:
+    """X_out[j] = blur(lognorm(img))[r2p[idx[j]], feat] without storing the
+    blurred slide: sample map → blur with the sample epilogue → copies for
+    repeated draws.  False (nothing done) when the fused kernel does not take
+    this shape; the caller then materialises the blur and gathers."""
+    H, W, C = img.shape
+    S, F = X_out.shape
+    if S == 0 or inv_mean is None:
+        return False
+    w = gaussian_taps(sigma, truncate)
+    r = (len(w) - 1) // 2
+    n = H * W
+    head = WS.get("sample_head", 4 * N.query("mw_sample_head_elems", n))
+    pix = WS.get("sample_pix", 4 * S)
+    st = stream()
+    with profiling.timed("sample_map", S * 16):
+        N.call("mw_sample_map", P(idx), P(r2p), S, n, P(head), P(pix), st)
+    with profiling.timed("blur_sample", n * C * img.element_size() + S * F * 4):
+        ok = N.try_call("mw_blur_sample", P(img), dtype_code(img), H, W, C, P(inv_mean),
+                        float(pseudoval), w.ctypes.data, r, P(head), S, P(feat), F, P(X_out), st)
+    if not ok:
+        return False
+    with profiling.timed("sample_fixup", S * 8):
+        N.call("mw_sample_fixup", P(pix), P(head), S, F, P(X_out), st)
+    FUSED_USED["sample"] += 1
+    return True
 
 
 def synth_slide(H, W, C, seed, mode="hard", n_seeds=32, n_domains=8, bg_frac=0.15):

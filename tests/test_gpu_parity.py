@@ -203,7 +203,22 @@ def _mxif_labeler_from(g, n):
     return M.mxif_labeler(df)
 
 
-def test_mxif_labeler_end_to_end_small(gpu, golden):
+@pytest.fixture(params=["0", "1"], ids=["materialised", "fused"])
+def blur_mode(request, monkeypatch):
+    """Run a pipeline test with the blurred slide materialised and with the
+    blur deferred into the fused sample / assign epilogues (MW_FUSED_BLUR);
+    in fused mode the fused kernels must actually have run."""
+    from milwrm_amd import device as D
+
+    monkeypatch.setenv("MW_FUSED_BLUR", request.param)
+    before = dict(D.FUSED_USED)
+    yield request.param
+    if request.param == "1":
+        assert D.FUSED_USED["sample"] > before["sample"], "fused sample epilogue not taken"
+        assert D.FUSED_USED["assign"] > before["assign"], "fused assign epilogue not taken"
+
+
+def test_mxif_labeler_end_to_end_small(gpu, golden, blur_mode):
     g = golden("mxif_small")
     lab = _mxif_labeler_from(g, 3)
     lab.prep_cluster_data(features=list(range(8)), sigma=2, fract=0.2)
@@ -226,7 +241,7 @@ def test_mxif_labeler_end_to_end_small(gpu, golden):
                                atol=1e-6)
 
 
-def test_mxif_labeler_hard256(gpu, golden):
+def test_mxif_labeler_hard256(gpu, golden, blur_mode):
     import milwrm_amd as M
 
     g = golden("mxif_hard256")
@@ -336,3 +351,53 @@ def test_device_mt19937_subsample_indices_bit_exact(gpu):
         ref = np.random.choice(777_777, 300_000)
         got, _ = subsample_indices_device(777_777, 300_000 / 777_777 + 1e-12, seed)
         np.testing.assert_array_equal(got.cpu().numpy(), ref)
+
+
+def _same_bits(a, b):
+    return bool(torch.equal(a.contiguous().view(torch.uint8), b.contiguous().view(torch.uint8)))
+
+
+@pytest.mark.parametrize("H,W,C,k,feats", [
+    (300, 260, 30, 8, None), (130, 64, 30, 16, None), (190, 210, 30, 8, [3, 1, 4, 15, 9, 2, 6]),
+    (200, 200, 16, 8, None), (160, 96, 64, 12, None), (1031, 778, 30, 8, None)])
+def test_fused_epilogues_match_materialised(gpu, H, W, C, k, feats):
+    """Blur with the sample / assign epilogue (blurred slide never stored) is
+    bit-identical to blur → gather and blur → assign: same X rows, column
+    statistics, labels, confidences and per-domain sums.  Parity of the
+    materialised path itself with the oracle is pinned by the tests above."""
+    from milwrm_amd import device as D
+    from milwrm_amd.assign import assign_image, blur_assign_image
+
+    raw, mask = D.synth_slide(H, W, C, seed=7, mode="hard")
+    mask = D.padded_mask(mask)
+    s, c = D.nz_stats(raw)
+    inv = (c.double() / s).float()
+    blurred = D.blur(raw, 2.0, inv_mean=inv)
+    r2p, M = D.mask_rank(mask.reshape(-1))
+    S = int(0.2 * M)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    idx = torch.randint(0, M, (S,), device="cuda", generator=g, dtype=torch.int32)
+    feats = list(range(C)) if feats is None else feats
+    F = len(feats)
+    feat = torch.tensor(feats, dtype=torch.int32, device="cuda")
+    X0 = torch.empty((S, F), dtype=torch.float32, device="cuda")
+    st0 = torch.zeros(2 * F + 1, dtype=torch.float64, device="cuda")
+    D.gather_rows(blurred, feat, idx, r2p, X0, st0, False)
+    X1 = torch.full((S, F), float("nan"), dtype=torch.float32, device="cuda")
+    assert D.blur_gather_fused(raw, 2.0, inv, 1.0, feat, idx, r2p, X1)
+    st1 = torch.zeros(2 * F + 1, dtype=torch.float64, device="cuda")
+    D.col_stats_rows(X1, st1, False)
+    assert _same_bits(X0, X1)
+    assert _same_bits(st0, st1)
+    if feats != list(range(C)):
+        return
+    mu = st0[1:1 + F].cpu().numpy()
+    invs = 1.0 / np.sqrt(st0[1 + F:].cpu().numpy() / st0[0].item())
+    rows = X0[torch.arange(0, S, max(1, S // k), device="cuda")[:k]].double().cpu().numpy()
+    centers = (rows - mu) * invs
+    l0, c0, d0 = assign_image(blurred, feats, mu, invs, centers, mask)
+    out = blur_assign_image(raw, 2.0, inv, 1.0, mu, invs, centers, mask)
+    assert out is not None
+    l1, c1, d1 = out
+    assert _same_bits(l0, l1) and _same_bits(c0, c1) and _same_bits(d0, d1)
