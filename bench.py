@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--channels", type=int, default=30)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--mode", default="hard", choices=["hard", "easy"])
-    ap.add_argument("--cpu-size", type=int, default=1536, help="oracle CPU-baseline slide side")
+    ap.add_argument("--cpu-size", type=int, default=2048, help="oracle CPU-baseline slide side")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -88,6 +88,27 @@ def cpu_baseline(size, C, k):
                 sample=f"oracle mxif_pipeline on one {size}x{size}x{C} synthetic slide, k={k} "
                        f"(n_iter {r['kmeans']['n_iter_']}), {dt:.1f} s, numpy/OpenBLAS threads="
                        f"{threads}")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3
+    FETCH_SIZE / WRITE_SIZE summary (profiles/*/pmc_traffic_*.json, written by
+    tools/pmc_traffic.py from run_pmc_bench.sh's separate counter passes over
+    this same bench command; corrections in that file)."""
+    import glob
+    import re
+
+    def ver(f):
+        m = re.search(r"r(\d+)/pmc_traffic_v(\d+)\.json$", f)
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic_v*.json")), key=ver)
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1])).get("kernels", {}).get(kernel)
+    if not rec or not rec.get("calibrated", False):
+        return None, None
+    return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -141,6 +162,7 @@ def main():
     dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
     per_launch_bytes = dom["bytes"] / max(dom["count"], 1)
     achieved = per_launch_bytes / (dom["mean_ms"] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dom_name)
     # SURVEY §8(d) whole-pipeline algorithmic bytes (per slide)
     N_pix, F, k = H * W, C, args.k
     B = (N_pix * C * 2 + (N_pix * C * 2 + N_pix + S * F * 4) + (k + n_iter + 1) * S * F * 4
@@ -165,7 +187,8 @@ def main():
                    "samples_per_slide": S, "lloyd_iters": n_iter, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-                     "traffic": None, "launches": dom["count"], "avg_launch_ms": dom["mean_ms"],
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "launches": dom["count"], "avg_launch_ms": dom["mean_ms"],
                      "algorithmic_bytes_per_launch": per_launch_bytes},
         "pipeline_roofline": {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,
                               "unit": "GB/s", "frac": pipe_gbps / (HBM_PEAK_GBPS * world)},

@@ -214,6 +214,18 @@ int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a,
                   uint8_t* d_labels, int mode, void* d_ws, void* stream);
 int mw_lloyd_reduce(const void* d_ws, int64_t S, int k, int F, double* d_out,
                     void* stream);
+/* n independent fits over the same rows in one pass (the k sweep of
+ * find_optimal_k, MILWRM.py:29-90): fit g has k = h_k[g] centers
+ * (d_centers[g], fp32 k x F), labels h_labels[g] and workspace h_ws[g]
+ * (mw_lloyd_ws_bytes(S, h_k[g], F)); the step is followed by the
+ * mw_lloyd_reduce of every fit into h_out[g].  Results are bitwise those of n
+ * separate mw_lloyd_step + mw_lloyd_reduce calls.  n <= 24; all fits of one
+ * call in the same class k <= 16 / 17..32 / 33..64. Host arrays of device
+ * pointers. */
+int mw_lloyd_step_multi(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
+                        int n, const float* const* h_centers, const int* h_k,
+                        uint8_t* const* h_labels, int mode, void* const* h_ws,
+                        double* const* h_out, void* stream);
 
 /* ---- empty-cluster relocation support (_k_means_common.pyx:181-226) ---------
  * fp64 distance of every row to centers[labels]; returns the n largest

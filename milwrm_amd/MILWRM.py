@@ -23,7 +23,7 @@ import torch
 
 from . import device as D
 from .assign import assign_image, assign_rows, blur_assign_image, domain_means
-from .kmeans import DeviceRows, KMeans, StandardScaler
+from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
 from .dist import LOCAL_COMM
@@ -52,7 +52,16 @@ def _inertia_o(rows: DeviceRows, comm=LOCAL_COMM) -> float:
 def chooseBestKforKMeansParallel(scaled_data, k_range, n_jobs=-1, comm=None, **kwargs):
     """MILWRM.py:57-90 (fits run one after another on the device)."""
     rows = scaled_data if isinstance(scaled_data, DeviceRows) else DeviceRows.from_host(scaled_data)
-    ans = [kMeansRes(rows, k, comm=comm, **kwargs) for k in k_range]
+    if os.environ.get("MW_SWEEP_BATCH", "1") == "0":  # one fit after another (A/B timing)
+        ans = [kMeansRes(rows, k, comm=comm, **kwargs) for k in k_range]
+    else:
+        # all k fitted together: one pass over the rows per Lloyd iteration
+        # for every fit still running (kmeans.fit_many); same values as kMeansRes
+        alpha_k = kwargs.get("alpha_k", 0.02)
+        inertia_o = _inertia_o(rows, LOCAL_COMM if comm is None else comm)
+        fits = fit_many(rows, list(k_range), random_state=kwargs.get("random_state", 18),
+                        comm=comm)
+        ans = [km.inertia_ / inertia_o + alpha_k * k for km, k in zip(fits, k_range)]
     ans = list(zip(k_range, ans))
     results = pd.DataFrame(ans, columns=["k", "Scaled Inertia"]).set_index("k")
     best_k = results.idxmin().iloc[0]
@@ -338,7 +347,7 @@ class mxif_labeler(tissue_labeler):
                 images.append(image)
         # phase 1: mask ranks → sample counts → one preallocated row block
         dev = D.device()
-        ranks = [D.mask_rank(im._mask_device().reshape(-1)) for im in images]
+        ranks = [im._mask_rank() for im in images]
         counts = [int(M * fract) for _, M in ranks]
         F = len(images[0]._features(features))
         X = torch.empty((sum(counts), F), dtype=torch.float32, device=dev)

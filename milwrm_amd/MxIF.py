@@ -143,6 +143,7 @@ class img:
     def mask(self, m):
         self._mask = m
         self._mask_dev = None
+        self._mrank = None
 
     def _mask_device(self) -> torch.Tensor:
         if self._mask_dev is None:
@@ -151,6 +152,19 @@ class img:
             m = np.ascontiguousarray(np.asarray(self._mask) != 0, dtype=np.uint8)
             self._mask_dev = D.padded_mask(torch.from_numpy(m).to(D.device()))
         return self._mask_dev
+
+    def _prefetch_mask_rank(self):
+        """Queue the mask rank on the stream without waiting for it (it only
+        depends on the mask): it then overlaps the host work between
+        calculate_non_zero_mean and subsample_pixels."""
+        if getattr(self, "_mrank", None) is None and self._mask is not None:
+            self._mrank = D.mask_rank_async(self._mask_device().reshape(-1))
+
+    def _mask_rank(self):
+        """(rank→pixel, M) of the current mask, from the prefetched launch if any."""
+        pending = getattr(self, "_mrank", None)
+        self._mrank = None
+        return D.mask_rank(self._mask_device().reshape(-1), pending)
 
     # -------------------------------------------------------------- basics
     def __repr__(self) -> str:
@@ -171,6 +185,7 @@ class img:
         new._dev = None if self._dev is None else self._dev.clone()
         new._mask = None if self._mask is None else self._mask.copy()
         new._mask_dev = None
+        new._mrank = None
         return new
 
     def _features(self, features):
@@ -207,6 +222,7 @@ class img:
         obj.ch = channels if channels is not None else ["ch_{}".format(x) for x in range(obj.n_ch)]
         obj._mask = None
         obj._mask_dev = None
+        obj._mrank = None
         if mask is not None:
             obj._mask = _DeviceMask(mask)
             obj._mask_dev = (mask != 0).to(torch.uint8) if mask.dtype != torch.uint8 else mask
@@ -332,7 +348,7 @@ class img:
         features = self._features(features)
         np.random.seed(random_state)  # the reference's global-RNG side effect (MxIF.py:484)
         src = D.as_float32(self._materialize())
-        r2p, M = D.mask_rank(self._mask_device().reshape(-1))
+        r2p, M = self._mask_rank()
         dev = src.device
         d_idx, total = subsample_indices_device(M, fract, random_state, dev)
         S = d_idx.shape[0]
@@ -366,6 +382,7 @@ class img:
         """MxIF.py:519-541: ([mean_c * pixels], pixels) with pixels = non-zero
         elements over all channels."""
         s, c = D.nz_stats(self._materialize())
+        self._prefetch_mask_rank()  # queued behind nz_stats, overlaps the host work that follows
         s = s.cpu().numpy()
         c = c.cpu().numpy()
         pixels = int(c.sum())

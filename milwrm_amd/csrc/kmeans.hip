@@ -543,12 +543,12 @@ __host__ __device__ inline size_t cent_t_bytes(int KS, int FMAX) {
 //           their MFMAs.  The record holds a*sum(x) + b*count = sum of scaled
 //           rows.
 template <int FMAX, int MB, int MODE>
-__global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_kernel(const float* __restrict__ X, int64_t S, int F,
-                                                    const float* __restrict__ ga,
-                                                    const float* __restrict__ gb,
-                                                    const float* __restrict__ gc, int k,
-                                                    uint8_t* __restrict__ labels,
-                                                    int64_t R, double* __restrict__ rec) {
+__device__ __forceinline__ void lloyd_body(const float* __restrict__ X, int64_t S, int F,
+                                           const float* __restrict__ ga,
+                                           const float* __restrict__ gb,
+                                           const float* __restrict__ gc, int k,
+                                           uint8_t* __restrict__ labels,
+                                           int64_t R, double* __restrict__ rec, const int blk) {
   constexpr int NV = FMAX / 4;                   // float4 per lane per tile
   constexpr int NB = FMAX <= 16 ? 1 : FMAX / 16;  // 16-feature MFMA column blocks
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -573,7 +573,7 @@ __global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_kernel(const float* _
     for (int q = t; q < k * F; q += blockDim.x) s_blk[q] = 0.0;
   __syncthreads();
 
-  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
+  const int64_t lo = (int64_t)blk * R, hi = min(S, lo + R);
   const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
   const int64_t total = S * (int64_t)F, n4 = total >> 2;
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + lo * F, (S - lo) * F * 4);
@@ -688,7 +688,7 @@ __global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_kernel(const float* _
   const double ch = block_sum((double)changed, s_red);
   const double in = block_sum(inert, s_red);
   const int rlen = lloyd_rec(k, F);
-  double* out = rec + (size_t)blockIdx.x * rlen;
+  double* out = rec + (size_t)blk * rlen;
   if (MODE == 0) {
     for (int w = 0; w < nw; ++w) {
       if (wid == w) {
@@ -724,11 +724,45 @@ __global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_kernel(const float* _
   }
 }
 
+template <int FMAX, int MB, int MODE>
+__global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_kernel(const float* __restrict__ X, int64_t S, int F,
+                                                    const float* __restrict__ ga,
+                                                    const float* __restrict__ gb,
+                                                    const float* __restrict__ gc, int k,
+                                                    uint8_t* __restrict__ labels,
+                                                    int64_t R, double* __restrict__ rec) {
+  lloyd_body<FMAX, MB, MODE>(X, S, F, ga, gb, gc, k, labels, R, rec, blockIdx.x);
+}
+
+// Several independent fits over the same rows in one launch (the
+// find_optimal_k sweep, MILWRM.py:29-90): block i runs fit i % n of row block
+// i / n, so the n blocks that read one row block are dispatched together and
+// all but the first find those rows in the on-die caches instead of HBM.
+// Per fit the arithmetic (row -> block map, per-block records, combine order)
+// is the single-fit kernel's: results are bitwise those of separate fits.
+constexpr int kMaxFits = 24;
+struct LloydFits {
+  const float* centers[kMaxFits];
+  uint8_t* labels[kMaxFits];
+  double* rec[kMaxFits];
+  double* out[kMaxFits];
+  int k[kMaxFits];
+};
+template <int FMAX, int MB, int MODE>
+__global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_multi_kernel(const float* __restrict__ X, int64_t S,
+                                                          int F, const float* __restrict__ ga,
+                                                          const float* __restrict__ gb,
+                                                          const LloydFits fits, int n, int64_t R) {
+  const int g = blockIdx.x % n, blk = blockIdx.x / n;
+  lloyd_body<FMAX, MB, MODE>(X, S, F, ga, gb, fits.centers[g], fits.k[g], fits.labels[g], R,
+                             fits.rec[g], blk);
+}
+
 // fixed-order sum of G per-block records: thread (q, part) sums blocks
 // b = part, part+8, ... with 8 independent partial sums, then parts combine
 // in order.
-__global__ void __launch_bounds__(256) lloyd_reduce_kernel(const double* __restrict__ rec, int G,
-                                                           int rl, double* __restrict__ out) {
+__device__ __forceinline__ void lloyd_reduce_body(const double* __restrict__ rec, int G, int rl,
+                                                  double* __restrict__ out) {
   __shared__ double s[8][33];
   const int lane = threadIdx.x & 31, part = threadIdx.x >> 5;  // 32 columns x 8 parts
   const int q = blockIdx.x * 32 + lane;
@@ -749,6 +783,18 @@ __global__ void __launch_bounds__(256) lloyd_reduce_kernel(const double* __restr
     for (int p2 = 0; p2 < 8; ++p2) t += s[p2][lane];
     out[q] = t;
   }
+}
+
+__global__ void __launch_bounds__(256) lloyd_reduce_kernel(const double* __restrict__ rec, int G,
+                                                           int rl, double* __restrict__ out) {
+  lloyd_reduce_body(rec, G, rl, out);
+}
+// one fit per blockIdx.y (records of lloyd_multi_kernel)
+__global__ void __launch_bounds__(256) lloyd_reduce_multi_kernel(const LloydFits fits, int G, int F) {
+  const int g = blockIdx.y, k = fits.k[g];
+  const int rl = lloyd_rec(k, F);
+  if ((int)blockIdx.x * 32 >= rl) return;  // block-uniform
+  lloyd_reduce_body(fits.rec[g], G, rl, fits.out[g]);
 }
 
 // ============================================================== farthest
@@ -1198,6 +1244,71 @@ int mw_lloyd_reduce(const void* d_ws, int64_t S, int k, int F, double* d_out, vo
   const int rl = lloyd_rec(k, F);
   hipLaunchKernelGGL(lloyd_reduce_kernel, dim3((rl + 31) / 32), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), kblocks(S), rl, d_out);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_lloyd_step_multi(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
+                        int n, const float* const* h_centers, const int* h_k,
+                        uint8_t* const* h_labels, int mode, void* const* h_ws, double* const* h_out,
+                        void* stream) {
+  MW_CHECK_ARG(d_X && d_a && d_b && h_centers && h_k && h_labels && h_ws && h_out,
+               "mw_lloyd_step_multi: null pointer");
+  MW_CHECK_ARG(S > 0 && F > 0 && n >= 1 && n <= kMaxFits, "mw_lloyd_step_multi: bad shape (n <= %d)",
+               kMaxFits);
+  MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_step_multi: bad mode");
+  LloydFits fits{};
+  int kmax = 0;
+  for (int g = 0; g < n; ++g) {
+    MW_CHECK_ARG(h_centers[g] && h_labels[g] && h_ws[g] && h_out[g] && h_k[g] >= 1,
+                 "mw_lloyd_step_multi: fit %d: bad arguments", g);
+    fits.centers[g] = h_centers[g];
+    fits.labels[g] = h_labels[g];
+    fits.rec[g] = reinterpret_cast<double*>(h_ws[g]);
+    fits.out[g] = h_out[g];
+    fits.k[g] = h_k[g];
+    kmax = h_k[g] > kmax ? h_k[g] : kmax;
+  }
+  if (kmax > 64 || F > 64) {
+    set_error("mw_lloyd_step_multi: k=%d F=%d unsupported (k <= 64, F <= 64)", kmax, F);
+    return MW_EUNSUPPORTED;
+  }
+  const int MBv = kmax <= 16 ? 1 : kmax <= 32 ? 2 : 4;
+  for (int g = 0; g < n; ++g)  // one M-step block shape per launch
+    if ((h_k[g] <= 16 ? 1 : h_k[g] <= 32 ? 2 : 4) != MBv) {
+      set_error("mw_lloyd_step_multi: fits mix k <= 16 / 17..32 / > 32 in one launch");
+      return MW_EINVAL;
+    }
+  hipStream_t s = as_stream(stream);
+  const int G = kblocks(S);
+  const int64_t R = krows(S);
+  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
+  const size_t cent = cent_t_bytes(64, FM);
+  const size_t blk = ((size_t)kmax * F * 8 + 15) & ~(size_t)15;
+  const size_t lds = cent + blk + 4 * lloyd_wave_bytes(FM);
+  const dim3 grid((unsigned)G * (unsigned)n);
+#define MW_LLM(FMV, MBV, MO)                                                                      \
+  hipLaunchKernelGGL((lloyd_multi_kernel<FMV, MBV, MO>), grid, dim3(256), lds, s, d_X, S, F, d_a, \
+                     d_b, fits, n, R)
+#define MW_LL(FMV, MBV)              \
+  if (mode == 0) MW_LLM(FMV, MBV, 0); \
+  else if (mode == 1) MW_LLM(FMV, 1, 1); \
+  else MW_LLM(FMV, 1, 2);
+#define MW_LLF(FMV)                \
+  if (MBv == 1) { MW_LL(FMV, 1) }     \
+  else if (MBv == 2) { MW_LL(FMV, 2) } \
+  else { MW_LL(FMV, 4) }
+  if (FM == 8) { MW_LLF(8) }
+  else if (FM == 16) { MW_LLF(16) }
+  else if (FM == 32) { MW_LLF(32) }
+  else { MW_LLF(64) }
+#undef MW_LLF
+#undef MW_LL
+#undef MW_LLM
+  MW_LAUNCH_CHECK();
+  const int rlmax = lloyd_rec(kmax, F);
+  hipLaunchKernelGGL(lloyd_reduce_multi_kernel, dim3((rlmax + 31) / 32, n), dim3(256), 0, s, fits, G,
+                     F);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

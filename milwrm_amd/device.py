@@ -163,14 +163,22 @@ def block_mean(img: torch.Tensor, fact: int):
     return out
 
 
-def mask_rank(mask_u8: torch.Tensor):
-    """(rank→pixel uint32 tensor of length M, M) for mask != 0 (row-major)."""
+def mask_rank_async(mask_u8: torch.Tensor):
+    """Launch the mask rank (no host sync): (rank→pixel int32 tensor of
+    length n, device count of mask != 0)."""
     n = mask_u8.numel()
     r2p = torch.empty(n, dtype=torch.int32, device=mask_u8.device)
     cnt = torch.empty(1, dtype=torch.int64, device=mask_u8.device)
     ws = WS.get("mrank", N.query("mw_mask_rank_ws_bytes", n))
     with profiling.timed("mask_rank", n):
         N.call("mw_mask_rank", P(mask_u8), n, P(r2p), P(cnt), P(ws), stream())
+    return r2p, cnt
+
+
+def mask_rank(mask_u8: torch.Tensor, pending=None):
+    """(rank→pixel int32 tensor of length M, M) for mask != 0 (row-major);
+    ``pending`` = an earlier mask_rank_async result for the same mask."""
+    r2p, cnt = mask_rank_async(mask_u8) if pending is None else pending
     M = int(cnt.item())
     return r2p[:M], M
 

@@ -239,6 +239,116 @@ def lloyd_device(rows: DeviceRows, centers_init: np.ndarray, max_iter=300, tol=0
     return labels, inertia, centers, i + 1
 
 
+def _mb_class(k: int) -> int:
+    return 1 if k <= 16 else 2 if k <= 32 else 4
+
+
+def lloyd_device_multi(rows: DeviceRows, inits, max_iter=300, tol=0.0, comm=LOCAL):
+    """``lloyd_device`` for several independent fits over the same rows, run in
+    lockstep: every iteration is ONE pass over the rows for all the fits
+    still running (``mw_lloyd_step_multi``, fits of one M-step class per
+    launch), one all-reduce and one device-to-host copy of all their records.
+    Each fit's arithmetic is the single-fit kernel's, so every fit returns
+    exactly what ``lloyd_device`` returns for it.  Returns a list of
+    (labels u8 tensor, inertia, centers fp64, n_iter)."""
+    S, F = rows.S, rows.F
+    dev = rows.X.device
+    n = len(inits)
+    ks = [int(np.asarray(c).shape[0]) for c in inits]
+    rls = [k * F + k + 2 for k in ks]
+    roff = np.concatenate([[0], np.cumsum(rls)]).astype(np.int64)
+    coff = np.concatenate([[0], np.cumsum([k * F for k in ks])]).astype(np.int64)
+    out_all = torch.zeros(int(roff[-1]), dtype=torch.float64, device=dev)
+    c32_all = torch.empty(int(coff[-1]), dtype=torch.float32, device=dev)
+    pin = torch.empty(int(coff[-1]), dtype=torch.float32, pin_memory=True)
+    labels = [torch.full((S,), 255, dtype=torch.uint8, device=dev) for _ in range(n)]
+    wss = [torch.empty(N.query("mw_lloyd_ws_bytes", S, k, F), dtype=torch.uint8, device=dev)
+           for k in ks]
+    centers = [np.array(c, dtype=np.float64) for c in inits]
+    done = [False] * n
+    strict = [False] * n
+    n_iter = [max_iter] * n
+    st = D.stream()
+    import ctypes
+
+    def launch(group, mode):
+        m = len(group)
+        P = ctypes.c_void_p * m
+        cp = P(*[D.P(c32_all) + int(coff[g]) * 4 for g in group])
+        kk = (ctypes.c_int * m)(*[ks[g] for g in group])
+        lp = P(*[D.P(labels[g]) for g in group])
+        wp = P(*[D.P(wss[g]) for g in group])
+        op = P(*[D.P(out_all) + int(roff[g]) * 8 for g in group])
+        nbytes = sum(S * (F * 4 + (2 if mode < 2 else 1)) for _ in group)
+        with profiling.timed(f"lloyd_multi_mode{mode}", nbytes):
+            N.call("mw_lloyd_step_multi", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), m,
+                   ctypes.addressof(cp), ctypes.addressof(kk), ctypes.addressof(lp), mode,
+                   ctypes.addressof(wp), ctypes.addressof(op), st)
+
+    def run(sel, mode_of):
+        """One pass for the fits in ``sel``; returns the host records."""
+        buf = pin.numpy()
+        for g in sel:
+            buf[coff[g]:coff[g + 1]] = centers[g].ravel()
+        c32_all.copy_(pin, non_blocking=True)
+        classes = {}
+        for g in sel:
+            classes.setdefault((mode_of(g), _mb_class(ks[g])), []).append(g)
+        for (mode, _), group in sorted(classes.items()):
+            for i in range(0, len(group), 24):
+                launch(group[i:i + 24], mode)
+        comm.all_reduce_(out_all)
+        return out_all.cpu().numpy()
+
+    for it in range(max_iter):
+        active = [g for g in range(n) if not done[g]]
+        if not active:
+            break
+        rec_all = run(active, lambda g: 0)
+        for g in active:
+            k = ks[g]
+            rec = rec_all[roff[g]:roff[g + 1]]
+            centers_new = rec[:k * F].reshape(k, F).copy()
+            weight = rec[k * F:k * F + k].copy()
+            changed = rec[k * F + k]
+            _relocate_empty(rows, labels[g], centers[g], centers_new, weight, comm)
+            _average_centers(centers_new, weight)
+            shift = np.sqrt(((centers_new - centers[g]) ** 2).sum(axis=1))
+            centers[g] = centers_new
+            if changed == 0:
+                strict[g], done[g], n_iter[g] = True, True, it + 1
+            elif (shift ** 2).sum() <= tol:
+                done[g], n_iter[g] = True, it + 1
+    rec_all = run(list(range(n)), lambda g: 2 if strict[g] else 1)
+    return [(labels[g], float(rec_all[roff[g] + ks[g] * F + ks[g] + 1]), centers[g], n_iter[g])
+            for g in range(n)]
+
+
+def fit_many(rows: DeviceRows, k_values, random_state=None, comm=None, **kw):
+    """``KMeans(n_clusters=k, random_state=random_state, **kw).fit(rows)`` for
+    every k, with the Lloyd iterations of all fits batched
+    (``lloyd_device_multi``); k-means++ seeding per fit as in ``KMeans.fit``.
+    Returns the fitted estimators (bitwise equal to separate fits)."""
+    comm = LOCAL if comm is None else comm
+    models, inits = [], []
+    for k in k_values:
+        km = KMeans(n_clusters=int(k), random_state=random_state, **kw)
+        km._check(rows.S)
+        if km.n_init not in ("auto", 1) or not isinstance(km.init, str) or km.init != "k-means++":
+            raise NotImplementedError("fit_many: k-means++ with a single init only")
+        km._tol = float(np.mean(rows.feature_var()) * km.tol) if km.tol else 0.0
+        c0, km.init_indices_ = km._kpp(rows, as_random_state(km.random_state), comm)
+        models.append(km)
+        inits.append(c0)
+    tols = {km._tol for km in models}
+    max_iters = {km.max_iter for km in models}
+    assert len(tols) == 1 and len(max_iters) == 1
+    res = lloyd_device_multi(rows, inits, max_iters.pop(), tols.pop(), comm)
+    for km, (labels, inertia, centers, n_iter) in zip(models, res):
+        km._set_fitted(rows, labels, inertia, centers, n_iter)
+    return models
+
+
 class KMeans:
     """Drop-in for ``sklearn.cluster.KMeans`` (lloyd) on the MI355X kernels.
 
@@ -308,10 +418,7 @@ class KMeans:
                                      f"match the number of clusters {k} / features {rows.F}.")
                 self.init_indices_ = None
             elif init == "k-means++":
-                if comm.sharded():
-                    centers0, self.init_indices_ = comm.kpp(rows, k, rs)
-                else:
-                    centers0, self.init_indices_ = _kmeans_plusplus_device(rows, k, rs)
+                centers0, self.init_indices_ = self._kpp(rows, rs, comm)
             elif init == "random":
                 if comm.sharded():
                     raise NotImplementedError("init='random' with sharded rows")
@@ -326,13 +433,20 @@ class KMeans:
                                                             self._tol, bool(self.verbose), comm)
             if best is None or inertia < best[1]:
                 best = (labels, inertia, centers, n_iter)
-        labels, inertia, centers, n_iter = best
+        return self._set_fitted(rows, *best)
+
+    def _kpp(self, rows, rs, comm):
+        if comm.sharded():
+            return comm.kpp(rows, int(self.n_clusters), rs)
+        return _kmeans_plusplus_device(rows, int(self.n_clusters), rs)
+
+    def _set_fitted(self, rows, labels, inertia, centers, n_iter):
         self._labels_dev = labels
         self.cluster_centers_ = centers
         self.inertia_ = inertia
         self.n_iter_ = n_iter
         self.n_features_in_ = rows.F
-        self._n_features_out = k
+        self._n_features_out = int(self.n_clusters)
         self._labels_host = None
         return self
 

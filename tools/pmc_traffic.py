@@ -1,0 +1,65 @@
+"""HBM traffic per launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
+run_pmc_bench.sh (gpurun_out/pmc_<tag>/{fetch,write}/run_counter_collection.csv)
+-> a JSON table bench.py reads for roofline.traffic.
+
+Corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section): both counters are
+in KB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced
+streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane
+streaming stores.  Kernels whose reads are not wide coalesced streams (the
+random-row gather) are uncalibrated and flagged as such.
+
+usage: python tools/pmc_traffic.py <tag> <out.json>
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+# bench.py profiling names -> substring of the HIP kernel symbol
+KERNELS = {
+    "blur": "blur_mfma_kernel<",
+    "assign_conf": "assign_kernel<",
+    "kpp_step": "kpp_dist_kernel<32, 4>",
+    "kpp_init": "kpp_dist_kernel<32, 1>",
+    "lloyd_step_mode0": "lloyd_kernel<32, 1, 0>",
+    "lloyd_step_mode1": "lloyd_kernel<32, 1, 1>",
+    "gather": "gather_kernel<",
+    "nz_stats": "nz_stats_kernel<",
+}
+UNCALIBRATED = {"gather"}  # 120-B random rows, not a wide coalesced stream
+
+
+def per_launch(path, pat):
+    tot = collections.defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if pat in r["Kernel_Name"]:
+            tot[r["Dispatch_Id"]] += float(r["Counter_Value"])
+    if not tot:
+        return None, 0
+    return sum(tot.values()) / len(tot), len(tot)
+
+
+def main():
+    tag, out = sys.argv[1], sys.argv[2]
+    base = f"gpurun_out/pmc_{tag}"
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
+                     f"'bench.py --steps 1 --warmup 1' ({base})",
+           "correction": "KB -> bytes; FETCH_SIZE x2 (gfx950 wide-read undercount); "
+                         "WRITE_SIZE as reported",
+           "kernels": {}}
+    for name, pat in KERNELS.items():
+        f, nf = per_launch(f"{base}/fetch/run_counter_collection.csv", pat)
+        w, nw = per_launch(f"{base}/write/run_counter_collection.csv", pat)
+        if f is None or w is None:
+            continue
+        fb, wb = 2 * f * 1024, w * 1024
+        res["kernels"][name] = {"symbol": pat, "launches": nf, "fetch_bytes": fb, "write_bytes": wb,
+                                "traffic_bytes": fb + wb, "calibrated": name not in UNCALIBRATED}
+    json.dump(res, open(out, "w"), indent=1)
+    for n, v in res["kernels"].items():
+        print(f"{n:18s} fetch {v['fetch_bytes'] / 1e9:8.3f} GB  write {v['write_bytes'] / 1e9:8.3f} GB")
+
+
+if __name__ == "__main__":
+    main()
