@@ -417,13 +417,12 @@ class mxif_labeler(tissue_labeler):
         """MILWRM.py:1868-1900 from the fused pass: confidence_IDs and the
         images x domains DataFrame of mean confidences."""
         k = self.kmeans.cluster_centers_.shape[0]
-        df = pd.DataFrame()
-        for i, dom in enumerate(self._dom_dev):
-            scores = domain_means(dom.cpu().numpy(), k)
-            d = pd.DataFrame(scores.values(), columns=[i])
-            df = pd.concat([df, d.T], ignore_index=True)
+        # images x domains, the frame the reference concatenates row by row
+        # (index 0..n-1, columns 0..k-1), built in one constructor call
+        doms = torch.stack(self._dom_dev).cpu().numpy() if self._dom_dev else np.zeros((0, 2 * k))
+        rows = [list(domain_means(dom, k).values()) for dom in doms]
         self.confidence_IDs = _LazyHostList(list(self._conf_dev), _conf_to_host)
-        self.confidence_score_df = df
+        self.confidence_score_df = pd.DataFrame(np.asarray(rows, dtype=np.float64).reshape(-1, k))
 
 
 class st_labeler(tissue_labeler):

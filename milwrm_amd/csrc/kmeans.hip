@@ -20,7 +20,10 @@
 namespace mw {
 
 #ifndef MW_LLOYD_WPS
-#define MW_LLOYD_WPS 1
+// waves per SIMD the Lloyd pass is compiled for: 3 for the F <= 32, k <= 16
+// instance (168 VGPRs, no spill; 6 % faster than 2 waves at 200 VGPRs),
+// 1 (no bound) for the larger tiles, which would spill
+#define MW_LLOYD_WPS ((FMAX <= 32 && MB == 1) ? 3 : 1)
 #endif
 #ifndef MW_ASSIGN_WPS
 #define MW_ASSIGN_WPS 1
@@ -418,7 +421,10 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // chain (even features in .x, odd in .y, then .x + .y) is the same fp32
 // operation sequence as a one-center loop, so the result does not depend on
 // the blocking.
-constexpr int kAhead = 3;
+#ifndef MW_KAHEAD
+#define MW_KAHEAD 1
+#endif
+constexpr int kAhead = MW_KAHEAD;  // center pairs in flight ahead of their FMAs
 template <int NP, int KS, int P>
 __device__ __forceinline__ void nc_read(uint32_t base, f2v (&c)[4]) {
   c[0] = ds_read8<P * KS * 8>(base);
@@ -653,6 +659,7 @@ __device__ __forceinline__ void lloyd_body(const float* __restrict__ X, int64_t 
       int bcol[NB];
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) bcol[nb] = min(16 * nb + jj, F - 1);  // cols >= F never read back
+#ifndef MW_X_NOM  // (ablation builds only: no M-step MFMAs)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {  // two batches of 8 k-steps (4 rows each)
         int Lr[8];
@@ -681,6 +688,7 @@ __device__ __forceinline__ void lloyd_body(const float* __restrict__ X, int64_t 
         for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc64[mb][nb][r] += (double)d[mb][nb][r];
+#endif
     }
   }
   // ---- block record (fixed combine order: waves in index order) ----
