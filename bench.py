@@ -141,11 +141,23 @@ def main():
     profiling.reset()
     profiling.enable(True)
     barrier()
+    prof_path = os.environ.get("MW_BENCH_CPROFILE")  # diagnostics: host profile of the timed steps
+    if prof_path:
+        import cProfile
+        cpr = cProfile.Profile()
+        cpr.enable()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         lab = step()
     barrier()
     elapsed = time.perf_counter() - t0
+    if prof_path:
+        cpr.disable()
+        cpr.dump_stats(f"{prof_path}.{rank}")
+        ms_ = torch.cuda.memory_stats()
+        print(json.dumps({k: ms_.get(k) for k in ("num_alloc_retries", "num_device_alloc",
+                                                  "num_device_free", "num_ooms")}),
+              file=sys.stderr, flush=True)
     profiling.enable(False)
     prof = profiling.summary()
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")

@@ -380,7 +380,7 @@ class mxif_labeler(tissue_labeler):
             self._images = images
         for tot, S in totals:
             check_total(tot, S)
-        st = comm.merge_stats(stats.cpu().numpy(), F)
+        st = comm.merge_stats(D.d2h(stats), F)
         self.scaler = StandardScaler.from_stats(st)
         mu, inv = self.scaler.affine()
         self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv)
@@ -419,7 +419,7 @@ class mxif_labeler(tissue_labeler):
         k = self.kmeans.cluster_centers_.shape[0]
         # images x domains, the frame the reference concatenates row by row
         # (index 0..n-1, columns 0..k-1), built in one constructor call
-        doms = torch.stack(self._dom_dev).cpu().numpy() if self._dom_dev else np.zeros((0, 2 * k))
+        doms = D.d2h(torch.stack(self._dom_dev)) if self._dom_dev else np.zeros((0, 2 * k))
         rows = [list(domain_means(dom, k).values()) for dom in doms]
         self.confidence_IDs = _LazyHostList(list(self._conf_dev), _conf_to_host)
         self.confidence_score_df = pd.DataFrame(np.asarray(rows, dtype=np.float64).reshape(-1, k))

@@ -383,8 +383,7 @@ class img:
         elements over all channels."""
         s, c = D.nz_stats(self._materialize())
         self._prefetch_mask_rank()  # queued behind nz_stats, overlaps the host work that follows
-        s = s.cpu().numpy()
-        c = c.cpu().numpy()
+        s, c = D.d2h(s, c)
         pixels = int(c.sum())
         with np.errstate(invalid="ignore", divide="ignore"):
             means = s / c

@@ -59,7 +59,7 @@ class DeviceRows:
 
     def scaled_rows(self, idx) -> np.ndarray:
         idx = torch.as_tensor(np.asarray(idx, dtype=np.int64), device=self.X.device)
-        x = self.X.index_select(0, idx).double().cpu().numpy()
+        x = D.d2h(self.X.index_select(0, idx).double())
         return (x - self.mu) * self.inv
 
     def to_host_scaled(self) -> np.ndarray:
@@ -138,7 +138,7 @@ def _kmeans_plusplus_device(rows: DeviceRows, k: int, random_state, n_local_tria
                    u.ctypes.data, T, D.P(ws), st)
     idx = torch.empty(k, dtype=torch.int64, device=rows.X.device)
     N.call("mw_kpp_indices", D.P(ws), S, T, k, D.P(idx), st)
-    idx = idx.cpu().numpy()
+    idx = D.d2h(idx).copy()
     idx[0] = first
     return rows.scaled_rows(idx), idx
 
@@ -198,20 +198,18 @@ def lloyd_device(rows: DeviceRows, centers_init: np.ndarray, max_iter=300, tol=0
     rl = k * F + k + 2
     out = torch.empty(rl, dtype=torch.float64, device=dev)
     c32 = torch.empty((k, F), dtype=torch.float32, device=dev)
-    pin = torch.empty((k, F), dtype=torch.float32, pin_memory=True)
     centers = np.array(centers_init, dtype=np.float64)
     strict = False
     st = D.stream()
 
     def step(mode):
-        pin.numpy()[:] = centers
-        c32.copy_(pin, non_blocking=True)
+        D.h2d_into(c32, centers.astype(np.float32))
         with profiling.timed(f"lloyd_step_mode{mode}", S * (F * 4 + (2 if mode < 2 else 1))):
             N.call("mw_lloyd_step", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(c32), k,
                    D.P(labels), mode, D.P(ws), st)
         N.call("mw_lloyd_reduce", D.P(ws), S, k, F, D.P(out), st)
         comm.all_reduce_(out)
-        return out.cpu().numpy()
+        return D.d2h(out)
 
     i = 0
     for i in range(max_iter):
@@ -260,7 +258,7 @@ def lloyd_device_multi(rows: DeviceRows, inits, max_iter=300, tol=0.0, comm=LOCA
     coff = np.concatenate([[0], np.cumsum([k * F for k in ks])]).astype(np.int64)
     out_all = torch.zeros(int(roff[-1]), dtype=torch.float64, device=dev)
     c32_all = torch.empty(int(coff[-1]), dtype=torch.float32, device=dev)
-    pin = torch.empty(int(coff[-1]), dtype=torch.float32, pin_memory=True)
+    host_c = np.zeros(int(coff[-1]), dtype=np.float32)
     labels = [torch.full((S,), 255, dtype=torch.uint8, device=dev) for _ in range(n)]
     wss = [torch.empty(N.query("mw_lloyd_ws_bytes", S, k, F), dtype=torch.uint8, device=dev)
            for k in ks]
@@ -287,10 +285,9 @@ def lloyd_device_multi(rows: DeviceRows, inits, max_iter=300, tol=0.0, comm=LOCA
 
     def run(sel, mode_of):
         """One pass for the fits in ``sel``; returns the host records."""
-        buf = pin.numpy()
         for g in sel:
-            buf[coff[g]:coff[g + 1]] = centers[g].ravel()
-        c32_all.copy_(pin, non_blocking=True)
+            host_c[coff[g]:coff[g + 1]] = centers[g].ravel()
+        D.h2d_into(c32_all, host_c)
         classes = {}
         for g in sel:
             classes.setdefault((mode_of(g), _mb_class(ks[g])), []).append(g)
@@ -298,7 +295,7 @@ def lloyd_device_multi(rows: DeviceRows, inits, max_iter=300, tol=0.0, comm=LOCA
             for i in range(0, len(group), 24):
                 launch(group[i:i + 24], mode)
         comm.all_reduce_(out_all)
-        return out_all.cpu().numpy()
+        return D.d2h(out_all)
 
     for it in range(max_iter):
         active = [g for g in range(n) if not done[g]]
