@@ -28,7 +28,7 @@ if has sweep; then
 fi
 if has prof; then
   echo "[gpu] rocprof"
-  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err" ) || { tail -5 "$R/gpurun_out/prof.err"; exit 1; }
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof.err" ) || { tail -5 "$R/gpurun_out/prof.err"; exit 1; }
 fi
 if has pmc; then
   echo "[gpu] pmc"
