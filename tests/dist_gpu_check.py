@@ -43,11 +43,21 @@ def main():
     res = dict(idx=lab.kmeans.init_indices_, n_iter=lab.kmeans.n_iter_,
                centers=lab.kmeans.cluster_centers_, inertia=lab.kmeans.inertia_,
                tid=np.nan_to_num(lab.tissue_IDs[0], nan=-1))
+    # k = 2..20 sweep (batched Lloyd, mw_lloyd_step_multi) on the sharded rows
+    lab.find_optimal_k(random_state=18, alpha=0.05)
+    res["best_k"] = int(lab.k)
+    res["curve"] = lab.inertia_curve_["Scaled Inertia"].values
     allres = [None] * world
     dist.all_gather_object(allres, res)
     ok = True
     if rank == 0:
         ref = labeler_for(slides, None)
+        ref_k = ref.k
+        ref.find_optimal_k(random_state=18, alpha=0.05)
+        ref_best = int(ref.k)
+        sweep_rel = float(np.max(np.abs(ref.inertia_curve_["Scaled Inertia"].values - allres[0]["curve"])
+                                 / ref.inertia_curve_["Scaled Inertia"].values))
+        ref.k = ref_k
         checks = {
             "init_indices": np.array_equal(ref.kmeans.init_indices_, allres[0]["idx"]),
             "n_iter": ref.kmeans.n_iter_ == allres[0]["n_iter"],
@@ -58,12 +68,14 @@ def main():
             "same_on_ranks": all(np.array_equal(a["centers"], allres[0]["centers"]) for a in allres),
             "labels": all(np.array_equal(np.nan_to_num(ref.tissue_IDs[r], nan=-1), allres[r]["tid"])
                           for r in range(world)),
+            "sweep_best_k": all(a["best_k"] == ref_best for a in allres),
+            "sweep_curve": sweep_rel < 1e-4,
         }
         ok = all(checks.values())
         print("dist_gpu_check", "PASS" if ok else "FAIL", checks,
               "inertia rel", abs(ref.kmeans.inertia_ - allres[0]["inertia"]) / ref.kmeans.inertia_,
               "centers abs", np.max(np.abs(ref.kmeans.cluster_centers_ - allres[0]["centers"])),
-              flush=True)
+              "sweep curve rel", sweep_rel, flush=True)
     flag = [ok]
     dist.broadcast_object_list(flag, src=0)
     dist.destroy_process_group()
