@@ -93,7 +93,7 @@ def cpu_baseline(size, C, k):
 def pmc_traffic(kernel):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3
     FETCH_SIZE / WRITE_SIZE summary (profiles/*/pmc_traffic_*.json, written by
-    tools/pmc_traffic.py from run_pmc_bench.sh's separate counter passes over
+    tools/pmc_traffic.py from tools/gpu/pmc_bench.sh's separate counter passes over
     this same bench command; corrections in that file)."""
     import glob
     import re

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counter passes (rocprofv3 --pmc, one pass per counter group, no tracing
-# domains) for a python command: bash run_pmc.sh <tag> <script.py> [args...]
+# domains) for a python command: bash tools/gpu/pmc_script.sh <tag> <script.py> [args...]
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
 TAG="$1"; shift

@@ -1,5 +1,7 @@
 #!/bin/bash
-# Session-6 GPU pass: parity tests, bench, rocprofv3 kernel stats, PMC HBM traffic passes.
+# GPU pass (STEPS=tests,dist,bench,sweep,prof,pmc): parity tests, 2-rank sharded check, bench,
+# k-sweep bench, rocprofv3 kernel stats, PMC HBM traffic passes; each step under its own limit.
+#   gpurun -- bash tools/gpu/round_pass.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -32,6 +34,6 @@ if has prof; then
 fi
 if has pmc; then
   echo "[gpu] pmc"
-  PMC_PASSES=fetch,write bash "$R/run_pmc_bench.sh" || exit 1
+  PMC_PASSES=fetch,write bash "$R/tools/gpu/pmc_bench.sh" || exit 1
 fi
 echo "[gpu] done"

@@ -1,5 +1,5 @@
 """HBM traffic per launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
-run_pmc_bench.sh (gpurun_out/pmc_<tag>/{fetch,write}/run_counter_collection.csv)
+tools/gpu/pmc_bench.sh (gpurun_out/pmc_<tag>/{fetch,write}/run_counter_collection.csv)
 -> a JSON table bench.py reads for roofline.traffic.
 
 Corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section): both counters are
