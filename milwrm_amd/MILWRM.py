@@ -287,9 +287,10 @@ class mxif_labeler(tissue_labeler):
         else:
             raise Exception("Image_df must be given with these columns in this format ['Img', "
                             "'batch_names', 'mean estimators', 'pixels']")
-        if self.image_df["Img"].apply(isinstance, args=[img]).all():
+        imgs = list(self.image_df["Img"])  # (the reference's Series.apply(isinstance).all())
+        if all(isinstance(x, img) for x in imgs):
             self.use_paths = False
-        elif self.image_df["Img"].apply(isinstance, args=[str]).all():
+        elif all(isinstance(x, str) for x in imgs):
             self.use_paths = True
         else:
             raise Exception("Img column in the dataframe should be either str for paths to the "
@@ -312,10 +313,17 @@ class mxif_labeler(tissue_labeler):
 
     def _batch_means(self, comm=LOCAL_COMM):
         """MILWRM.py:1706-1714 (summed over ranks when sharded)."""
+        # per batch, in order of first appearance: sum of the images' estimator
+        # arrays and pixel counts, accumulated in row order from 0 exactly as
+        # the reference's sum(map(np.array, ...)) / sum(Series) over its
+        # boolean selection (one pass instead of a selection per batch)
         per = {}
-        for batch in self.image_df["batch_names"].unique():
-            sel = self.image_df[self.image_df["batch_names"] == batch]
-            per[batch] = (sum(map(np.array, list(sel["mean estimators"]))), sum(sel["pixels"]))
+        df = self.image_df
+        for batch, est, px in zip(df["batch_names"], df["mean estimators"], df["pixels"]):
+            acc = per.setdefault(batch, [0, 0])
+            acc[0] = acc[0] + np.array(est)
+            acc[1] = acc[1] + px
+        per = {b: (e, p) for b, (e, p) in per.items()}
         if comm.sharded():
             per = comm.sum_batches(per)
         return {b: est / pixels for b, (est, pixels) in per.items()}

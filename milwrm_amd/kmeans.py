@@ -334,7 +334,9 @@ def fit_many(rows: DeviceRows, k_values, random_state=None, comm=None, **kw):
         if km.n_init not in ("auto", 1) or not isinstance(km.init, str) or km.init != "k-means++":
             raise NotImplementedError("fit_many: k-means++ with a single init only")
         km._tol = float(np.mean(rows.feature_var()) * km.tol) if km.tol else 0.0
-        c0, km.init_indices_ = km._kpp(rows, as_random_state(km.random_state), comm)
+        seeded = isinstance(km.random_state, (int, np.integer)) and not isinstance(km.random_state, bool)
+        c0, km.init_indices_ = km._kpp(rows, km.random_state if seeded else
+                                       as_random_state(km.random_state), comm)
         models.append(km)
         inits.append(c0)
     tols = {km._tol for km in models}
@@ -405,7 +407,13 @@ class KMeans:
             warnings.warn(f"Explicit initial center position passed: performing only one init in "
                           f"KMeans instead of n_init={n_init}.", RuntimeWarning, stacklevel=2)
             n_init = 1
-        rs = as_random_state(self.random_state)
+        rs_box = []
+
+        def rs():  # created on first use (a seeded single k-means++ init never needs it)
+            if not rs_box:
+                rs_box.append(as_random_state(self.random_state))
+            return rs_box[0]
+
         best = None
         for _ in range(n_init):
             if arraylike:
@@ -415,11 +423,16 @@ class KMeans:
                                      f"match the number of clusters {k} / features {rows.F}.")
                 self.init_indices_ = None
             elif init == "k-means++":
-                centers0, self.init_indices_ = self._kpp(rows, rs, comm)
+                # a single init from an int seed draws from a fresh
+                # RandomState(seed): pass the seed (memoised draws, rng.kpp_draws)
+                seeded = n_init == 1 and isinstance(self.random_state, (int, np.integer)) \
+                    and not isinstance(self.random_state, bool)
+                centers0, self.init_indices_ = self._kpp(rows, self.random_state if seeded else rs(),
+                                                         comm)
             elif init == "random":
                 if comm.sharded():
                     raise NotImplementedError("init='random' with sharded rows")
-                seeds = rs.choice(rows.S, size=k, replace=False,
+                seeds = rs().choice(rows.S, size=k, replace=False,
                                   p=np.full(rows.S, 1.0 / rows.S))
                 centers0, self.init_indices_ = rows.scaled_rows(seeds), seeds
             elif callable(init):
