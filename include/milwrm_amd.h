@@ -262,6 +262,19 @@ int mw_domain_records(const int8_t* d_label, const float* d_conf, int64_t n_pix,
 int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom,
                      void* stream);
 
+/* ---- clustering QC statistics ------------------------------------------------
+ * Replaces the per-domain loops of estimate_percentage_variance_mxif
+ * (MILWRM.py:280-333, dc/dm sums) and estimate_mse_mxif (MILWRM.py:453-515).
+ * Over n_pix HWC fp32 pixels, x' = x[feat[f]]*a[f] + b[f] (fp64):
+ * d_out (fp64, M = k*F + 2F + k) = [sum over label==d of (x'_f - c_df)^2 (k x F)
+ * | sum x'_f (F) | sum x'_f^2 (F, over every pixel) | pixel count per label (k)].
+ * Labels outside [0, k) (masked / NaN tissue_ID → -1) add to the sums only.
+ * 1 <= k <= 20, 1 <= F <= 256; deterministic (fixed fold order). */
+size_t mw_domain_sse_ws_bytes(int64_t n_pix, int k, int F);
+int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
+                  const double* d_b, const double* d_centers, int k, const int8_t* d_label,
+                  int64_t n_pix, double* d_out, void* d_ws, void* stream);
+
 /* ---- synthetic slide generator (benchmark input; SURVEY §8d shape) ----------
  * uint16 HWC + uint8 mask: Voronoi domains (seeds given), per-domain channel
  * profiles, gamma-like multiplicative noise from a counter-based hash. */

@@ -22,7 +22,7 @@ import pandas as pd
 import torch
 
 from . import device as D
-from .assign import assign_image, assign_rows, blur_assign_image, domain_means
+from .assign import assign_image, assign_rows, blur_assign_image, domain_means, domain_sse_image
 from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
@@ -141,6 +141,36 @@ def estimate_confidence_score_st(sub_cluster_data, adata, centroids):
         else:
             mean_conf_score[i] = np.nan
     return mean_conf_score
+
+
+def _domain_stats(image, use_path, scaler, centroids, features, tissue_ID):
+    if use_path:
+        image = img.from_npz(image + ".npz")
+    feats = image._features(features)
+    mu, inv = scaler.affine()
+    src = D.as_float32(image._materialize())
+    return domain_sse_image(src, feats, mu, inv, np.asarray(centroids, dtype=np.float64),
+                            tissue_ID)
+
+
+def estimate_percentage_variance_mxif(image, use_path, scaler, centroids, features, tissue_ID):
+    """MILWRM.py:280-333: 100 * sum over domains of (x' - c)^2 / sum over the
+    whole slide of (x' - mean(x'))^2, from one ``mw_domain_sse`` pass."""
+    s = _domain_stats(image, use_path, scaler, centroids, features, tissue_ID)
+    dm = float(np.sum(s["sumsq"] - s["sum"] * s["sum"] / s["n"]))
+    return float(np.sum(s["sse"])) / dm * 100
+
+
+def estimate_mse_mxif(images, use_path, tissue_IDs, scaler, centroids, features, k):
+    """MILWRM.py:453-515: {domain: [per-feature MSE for each image]} (zeros for
+    a domain an image does not hold)."""
+    centroids = np.asarray(centroids, dtype=np.float64)[:k]
+    mse_temp = []
+    for image, tid in zip(images, tissue_IDs):
+        s = _domain_stats(image, use_path, scaler, centroids, features, tid)
+        cnt = s["count"][:, None]
+        mse_temp.append(np.where(cnt > 0, s["sse"] / np.maximum(cnt, 1), 0.0))
+    return {i: [m[i] for m in mse_temp] for i in range(k)} if len(images) else {}
 
 
 def _assign_img(image: img, features, centers, scaler):

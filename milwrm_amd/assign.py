@@ -75,6 +75,51 @@ def blur_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: floa
     return lab, conf, dom
 
 
+def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
+                     tissue_id) -> dict:
+    """Per-domain squared error and whole-slide scaled sums in one pass
+    (``mw_domain_sse``; the sums behind ``estimate_percentage_variance_mxif``
+    MILWRM.py:280-333 and ``estimate_mse_mxif`` MILWRM.py:453-515).
+
+    ``tissue_id``: H x W labels as the reference holds them (float, NaN outside
+    the mask) or an int8 device map with -1 outside the mask.  Returns fp64
+    host arrays: sse (k x F), sum (F), sumsq (F), count (k), n (pixels)."""
+    H, W, C = img_f32.shape
+    k, F = centers.shape
+    if not 1 <= k <= 20:
+        raise ValueError(f"domain statistics support 1 <= k <= 20 domains, got {k}")
+    img_f32 = img_f32.contiguous()
+    feat = np.asarray(feat_idx, dtype=np.int32)
+    feat = np.where(feat < 0, feat + C, feat).astype(np.int32)
+    if feat.shape != (F,) or feat.min() < 0 or feat.max() >= C:
+        raise ValueError(f"features {feat_idx} do not match {F} centroid columns / {C} channels")
+    dev = img_f32.device
+    n = H * W
+    if isinstance(tissue_id, torch.Tensor) and tissue_id.dtype == torch.int8:
+        lab = tissue_id.to(dev).reshape(n).contiguous()
+    else:
+        t = np.asarray(tissue_id, dtype=np.float64).reshape(-1)
+        if t.size != n:
+            raise ValueError(f"tissue_ID has {t.size} pixels, image has {n}")
+        ok = np.isfinite(t) & (t >= 0) & (t < k) & (t == np.floor(t))
+        lab = D.h2d(np.where(ok, t, -1).astype(np.int8), dev)
+    inv = np.asarray(inv, dtype=np.float64)
+    a = D.h2d(inv, dev)
+    b = D.h2d(-np.asarray(mu, dtype=np.float64) * inv, dev)
+    c64 = D.h2d(np.ascontiguousarray(centers, dtype=np.float64), dev)
+    feat_d = D.h2d(feat, dev)
+    M = k * F + 2 * F + k
+    out = torch.empty(M, dtype=torch.float64, device=dev)
+    ws = D.WS.get("domain_sse", N.query("mw_domain_sse_ws_bytes", n, k, F))
+    st = D.stream()
+    with profiling.timed("domain_sse", n * (C * 4 + 1)):
+        N.call("mw_domain_sse", D.P(img_f32), C, D.P(feat_d), F, D.P(a), D.P(b), D.P(c64),
+               k, D.P(lab), n, D.P(out), D.P(ws), st)
+    o = out.cpu().numpy()
+    return {"sse": o[:k * F].reshape(k, F), "sum": o[k * F:k * F + F],
+            "sumsq": o[k * F + F:k * F + 2 * F], "count": o[k * F + 2 * F:], "n": n}
+
+
 def assign_rows(X: np.ndarray, centers: np.ndarray, mu=None, inv=None):
     """Assign host rows (S x F, already in the centers' space unless an
     affine is given).  Returns (labels int64, conf fp64, dom fp64[2k])."""

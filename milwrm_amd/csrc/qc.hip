@@ -1,0 +1,132 @@
+// Clustering QC statistics: per-domain squared error against the centroids and
+// the whole-slide scaled sums, in one streaming pass over an HWC fp32 slide.
+//
+// Serves `estimate_percentage_variance_mxif` (MILWRM.py:280-333) and
+// `estimate_mse_mxif` (MILWRM.py:453-515): both scale the feature channels
+// with the StandardScaler (x' = x*a + b, a = 1/scale, b = -mean/scale), then
+//   dc   = sum over pixels with tissue_ID == d of (x'_f - c_df)^2   (per d, f)
+//   dm   = sum over ALL pixels of (x'_f - mean_f(x'))^2             (per f)
+// dm is recovered on the host from the per-feature sums of x' and x'^2.
+// Masked-out pixels (tissue_ID NaN → label -1 here) add to dm only, as in the
+// reference (`tissue_ID == i` is false for NaN).
+//
+// Layout: a block of 256 threads is split into floor(256/F) groups of F lanes;
+// lane f of a group owns feature f, so a wave reads whole pixels (F contiguous
+// floats for identity features) and every lane keeps its own per-domain
+// column of fp64 accumulators in LDS (no atomics, no bank conflicts).  Per
+// block partials go to a workspace and a second kernel folds them in block
+// order, so the result is deterministic.  HBM-bound: n_pix * (C*4 + 1) bytes.
+#include "common.h"
+
+namespace mw {
+
+constexpr int kQcThreads = 256;
+constexpr int kQcMaxK = 20;  // LDS: 20*256*(8+4) + 2*256*8 = 64 KiB, the default dynamic limit
+constexpr int kQcMaxBlocks = 1024;
+
+__global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
+    const float* __restrict__ img, int C, const int32_t* __restrict__ feat, int F,
+    const double* __restrict__ a, const double* __restrict__ b, const double* __restrict__ centers,
+    int k, const int8_t* __restrict__ label, int64_t n_pix, int M, double* __restrict__ part) {
+  extern __shared__ double lds[];
+  double* sse = lds;                                           // [k][256]
+  double* s1s = sse + (size_t)k * kQcThreads;                  // [256]
+  double* s2s = s1s + kQcThreads;                              // [256]
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(s2s + kQcThreads);  // [k][256]
+  const int t = threadIdx.x;
+  const int groups = kQcThreads / F;
+  const int g = t / F, f = t - g * F;
+  for (int d = 0; d < k; ++d) {
+    sse[d * kQcThreads + t] = 0.0;
+    cnt[d * kQcThreads + t] = 0u;
+  }
+  double s1 = 0.0, s2 = 0.0;
+  if (g < groups) {
+    const int ch = feat[f];
+    const double af = a[f], bf = b[f];
+    const int64_t step = (int64_t)gridDim.x * groups;
+    for (int64_t p = (int64_t)blockIdx.x * groups + g; p < n_pix; p += step) {
+      const double x = (double)img[p * C + ch] * af + bf;
+      s1 += x;
+      s2 += x * x;
+      const int l = label[p];
+      if (l >= 0 && l < k) {
+        const double dd = x - centers[l * F + f];
+        sse[l * kQcThreads + t] += dd * dd;
+        if (f == 0) cnt[l * kQcThreads + t] += 1u;
+      }
+    }
+  }
+  s1s[t] = s1;
+  s2s[t] = s2;
+  __syncthreads();
+  // fold the groups: output [sse k*F | sum F | sumsq F | count k]
+  for (int e = t; e < M; e += kQcThreads) {
+    double r = 0.0;
+    if (e < k * F) {
+      const int d = e / F, ff = e - d * F;
+      for (int gg = 0; gg < groups; ++gg) r += sse[d * kQcThreads + gg * F + ff];
+    } else if (e < k * F + F) {
+      const int ff = e - k * F;
+      for (int gg = 0; gg < groups; ++gg) r += s1s[gg * F + ff];
+    } else if (e < k * F + 2 * F) {
+      const int ff = e - k * F - F;
+      for (int gg = 0; gg < groups; ++gg) r += s2s[gg * F + ff];
+    } else {
+      const int d = e - k * F - 2 * F;
+      for (int gg = 0; gg < groups; ++gg) r += (double)cnt[d * kQcThreads + gg * F];
+    }
+    part[(size_t)blockIdx.x * M + e] = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void domain_sse_reduce(const double* __restrict__ part, int G,
+                                                         int M, double* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= M) return;
+  double r = 0.0;
+  for (int i = 0; i < G; ++i) r += part[(size_t)i * M + e];
+  out[e] = r;
+}
+
+static int qc_blocks(int64_t n_pix, int F) {
+  const int groups = kQcThreads / F;
+  const int64_t want = (n_pix + (int64_t)groups * 64 - 1) / ((int64_t)groups * 64);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, kQcMaxBlocks));
+}
+
+}  // namespace mw
+
+using namespace mw;
+
+extern "C" {
+
+size_t mw_domain_sse_ws_bytes(int64_t n_pix, int k, int F) {
+  if (n_pix <= 0 || k <= 0 || F <= 0 || F > kQcThreads) return 0;
+  const int M = k * F + 2 * F + k;
+  return (size_t)qc_blocks(n_pix, F) * M * sizeof(double);
+}
+
+int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
+                  const double* d_b, const double* d_centers, int k, const int8_t* d_label,
+                  int64_t n_pix, double* d_out, void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_img && d_feat && d_a && d_b && d_centers && d_label && d_out && d_ws,
+               "mw_domain_sse: null pointer");
+  MW_CHECK_ARG(n_pix > 0 && C > 0 && F > 0 && F <= kQcThreads && k >= 1 && k <= kQcMaxK,
+               "mw_domain_sse: bad shape n_pix=%lld C=%d F=%d k=%d (F <= 256, k <= 20)",
+               (long long)n_pix, C, F, k);
+  hipStream_t st = as_stream(stream);
+  const int G = qc_blocks(n_pix, F);
+  const int M = k * F + 2 * F + k;
+  const size_t lds = (size_t)k * kQcThreads * (sizeof(double) + sizeof(uint32_t)) +
+                     2 * kQcThreads * sizeof(double);
+  double* part = reinterpret_cast<double*>(d_ws);
+  hipLaunchKernelGGL(domain_sse_kernel, dim3(G), dim3(kQcThreads), lds, st, d_img, C, d_feat, F,
+                     d_a, d_b, d_centers, k, d_label, n_pix, M, part);
+  MW_LAUNCH_CHECK();
+  hipLaunchKernelGGL(domain_sse_reduce, dim3((M + 255) / 256), dim3(256), 0, st, part, G, M, d_out);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+}  // extern "C"

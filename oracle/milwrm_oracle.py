@@ -420,6 +420,32 @@ def confidence_mxif(img_hwc, mask, features, centers, mean, scale, tissue_id):
     return cid, means
 
 
+def percentage_variance_mxif(img_hwc, features, centers, mean, scale, tissue_id):
+    """``estimate_percentage_variance_mxif`` (MILWRM.py:280-333)."""
+    x = np.asarray(img_hwc, dtype=np.float64)[:, :, features]
+    h, w, d = x.shape
+    xs = scaler_transform(x.reshape(h * w, d), mean, scale)
+    tid = np.asarray(tissue_id).reshape(h * w)
+    dc = np.zeros(xs.shape)
+    for i in range(centers.shape[0]):
+        dc[tid == i] = (xs[tid == i] - centers[i]) ** 2
+    dm = (xs - xs.mean(axis=0)) ** 2
+    return np.sum(dc) / np.sum(dm) * 100
+
+
+def mse_mxif(imgs, tissue_ids, features, centers, mean, scale, k):
+    """``estimate_mse_mxif`` (MILWRM.py:453-515)."""
+    out = {}
+    for im, ar in zip(imgs, tissue_ids):
+        x = np.asarray(im, dtype=np.float64)[:, :, features]
+        h, w, d = x.shape
+        xs = scaler_transform(x.reshape(h * w, d), mean, scale).reshape(h, w, d)
+        for i in range(k):
+            v = (xs[ar == i] - centers[i]) ** 2
+            out.setdefault(i, []).append(np.zeros(centers.shape[1]) if len(v) == 0 else v.mean(axis=0))
+    return out
+
+
 def confidence_st(X, centers, labels):
     """``estimate_confidence_score_st`` (MILWRM.py:557-598)."""
     X = np.asarray(X, dtype=np.float64)

@@ -452,3 +452,50 @@ def test_fused_epilogues_match_materialised(gpu, H, W, C, k, feats):
     assert out is not None
     l1, c1, d1 = out
     assert _same_bits(l0, l1) and _same_bits(c0, c1) and _same_bits(d0, d1)
+
+
+class _Scaler:
+    def __init__(self, mean, scale):
+        self.mean_, self.scale_ = mean, scale
+
+    def affine(self):
+        return self.mean_.copy(), 1.0 / self.scale_
+
+
+@pytest.mark.parametrize("H,W,C,k,feats", [(64, 48, 8, 5, None), (97, 131, 30, 8, [0, 3, 5, 7, 11, 29]),
+                                           (33, 17, 12, 20, [2, -1])])
+def test_qc_estimators(gpu, H, W, C, k, feats):
+    """estimate_percentage_variance_mxif / estimate_mse_mxif (MILWRM.py:280-333,
+    453-515) through mw_domain_sse against the oracle's restatement: masked
+    (NaN) pixels, an empty domain, a feature subset and k at the kernel's limit.
+    fp64 sums over fp32 pixels: rtol 1e-8."""
+    import milwrm_amd as M
+    from milwrm_amd import MILWRM as MW
+
+    rng = np.random.default_rng(H * W + C)
+    fidx = list(range(C)) if feats is None else [f % C for f in feats]
+    F = len(fidx)
+    arrs, tids = [], []
+    mean = rng.random(F) * 1.5
+    scale = 0.5 + rng.random(F)
+    centers = rng.standard_normal((k, F))
+    for j in range(2):
+        arr = (rng.random((H, W, C)) * 3).astype(np.float32)
+        mask = (rng.random((H, W)) > 0.2).astype(np.uint8)
+        tid = O.tissue_ids(arr, mask, fidx, centers, mean, scale)
+        tid[tid == 1] = 0  # domain 1 empty: MSE row of zeros
+        arrs.append(arr)
+        tids.append(tid)
+    ims = [M.img(a.copy(), mask=np.ones((H, W), dtype=np.uint8)) for a in arrs]
+    sc = _Scaler(mean, scale)
+    for im, a, t in zip(ims, arrs, tids):
+        got = MW.estimate_percentage_variance_mxif(im, False, sc, centers, feats, t)
+        ref = O.percentage_variance_mxif(a, fidx, centers, mean, scale, t)
+        assert abs(got - ref) <= 1e-8 * abs(ref), (got, ref)
+    got = MW.estimate_mse_mxif(ims, False, tids, sc, centers, feats, k)
+    ref = O.mse_mxif(arrs, tids, fidx, centers, mean, scale, k)
+    assert sorted(got) == sorted(ref) == list(range(k))
+    for i in range(k):
+        for g_, r_ in zip(got[i], ref[i]):
+            np.testing.assert_allclose(g_, r_, rtol=1e-8, atol=1e-12)
+    assert all(np.all(v == 0) for v in got[1])
