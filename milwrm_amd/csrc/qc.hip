@@ -13,16 +13,16 @@
 // Layout: a block of 256 threads is split into floor(256/F) groups of F lanes;
 // lane f of a group owns feature f, so a wave reads whole pixels (F contiguous
 // floats for identity features) and every lane keeps its own per-domain
-// column of fp64 accumulators in LDS (no atomics, no bank conflicts).  Per
-// block partials go to a workspace and a second kernel folds them in block
-// order, so the result is deterministic.  HBM-bound: n_pix * (C*4 + 1) bytes.
+// column of fp64 accumulators in LDS (no atomics, no bank conflicts); four
+// pixels' loads are issued before their updates.  Per-block partials go to a
+// workspace and a second kernel folds them in a fixed order (deterministic).  HBM-bound: n_pix * (C*4 + 1) bytes.
 #include "common.h"
 
 namespace mw {
 
 constexpr int kQcThreads = 256;
-constexpr int kQcMaxK = 20;  // LDS: 20*256*(8+4) + 2*256*8 = 64 KiB, the default dynamic limit
-constexpr int kQcMaxBlocks = 1024;
+constexpr int kQcMaxK = 20;  // LDS <= 20*256*8 + 2*256*8 + 20*256*4 (F = 1) = 64 KiB, the default limit
+constexpr int kQcMaxBlocks = 2048;
 
 __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
     const float* __restrict__ img, int C, const int32_t* __restrict__ feat, int F,
@@ -32,30 +32,42 @@ __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
   double* sse = lds;                                           // [k][256]
   double* s1s = sse + (size_t)k * kQcThreads;                  // [256]
   double* s2s = s1s + kQcThreads;                              // [256]
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(s2s + kQcThreads);  // [k][256]
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(s2s + kQcThreads);  // [k][groups]
   const int t = threadIdx.x;
   const int groups = kQcThreads / F;
   const int g = t / F, f = t - g * F;
-  for (int d = 0; d < k; ++d) {
-    sse[d * kQcThreads + t] = 0.0;
-    cnt[d * kQcThreads + t] = 0u;
-  }
+  for (int d = 0; d < k; ++d) sse[d * kQcThreads + t] = 0.0;
+  for (int i = t; i < k * groups; i += kQcThreads) cnt[i] = 0u;
+  __syncthreads();
   double s1 = 0.0, s2 = 0.0;
   if (g < groups) {
     const int ch = feat[f];
     const double af = a[f], bf = b[f];
     const int64_t step = (int64_t)gridDim.x * groups;
-    for (int64_t p = (int64_t)blockIdx.x * groups + g; p < n_pix; p += step) {
-      const double x = (double)img[p * C + ch] * af + bf;
+    auto add = [&](float v, int l) {
+      const double x = (double)v * af + bf;
       s1 += x;
       s2 += x * x;
-      const int l = label[p];
       if (l >= 0 && l < k) {
         const double dd = x - centers[l * F + f];
         sse[l * kQcThreads + t] += dd * dd;
-        if (f == 0) cnt[l * kQcThreads + t] += 1u;
+        if (f == 0) cnt[l * groups + g] += 1u;
       }
+    };
+    int64_t p = (int64_t)blockIdx.x * groups + g;
+    // four pixels' loads in flight before their (LDS read-modify-write) updates
+    for (; p + 3 * step < n_pix; p += 4 * step) {
+      float v[4];
+      int l[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = img[(p + u * step) * C + ch];
+        l[u] = label[p + u * step];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(v[u], l[u]);
     }
+    for (; p < n_pix; p += step) add(img[p * C + ch], label[p]);
   }
   s1s[t] = s1;
   s2s[t] = s2;
@@ -74,19 +86,22 @@ __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
       for (int gg = 0; gg < groups; ++gg) r += s2s[gg * F + ff];
     } else {
       const int d = e - k * F - 2 * F;
-      for (int gg = 0; gg < groups; ++gg) r += (double)cnt[d * kQcThreads + gg * F];
+      for (int gg = 0; gg < groups; ++gg) r += (double)cnt[d * groups + gg];
     }
     part[(size_t)blockIdx.x * M + e] = r;
   }
 }
 
+// One workgroup per output element: lane i sums blocks i, i+256, ... in order,
+// then a fixed-order block tree (deterministic).
 __global__ __launch_bounds__(256) void domain_sse_reduce(const double* __restrict__ part, int G,
                                                          int M, double* __restrict__ out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= M) return;
+  __shared__ double scratch[256 / kWave];
+  const int e = blockIdx.x;
   double r = 0.0;
-  for (int i = 0; i < G; ++i) r += part[(size_t)i * M + e];
-  out[e] = r;
+  for (int i = threadIdx.x; i < G; i += 256) r += part[(size_t)i * M + e];
+  r = block_sum(r, scratch);
+  if (threadIdx.x == 0) out[e] = r;
 }
 
 static int qc_blocks(int64_t n_pix, int F) {
@@ -118,13 +133,13 @@ int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const
   hipStream_t st = as_stream(stream);
   const int G = qc_blocks(n_pix, F);
   const int M = k * F + 2 * F + k;
-  const size_t lds = (size_t)k * kQcThreads * (sizeof(double) + sizeof(uint32_t)) +
-                     2 * kQcThreads * sizeof(double);
+  const size_t lds = (size_t)k * kQcThreads * sizeof(double) + 2 * kQcThreads * sizeof(double) +
+                     (size_t)k * (kQcThreads / F) * sizeof(uint32_t);
   double* part = reinterpret_cast<double*>(d_ws);
   hipLaunchKernelGGL(domain_sse_kernel, dim3(G), dim3(kQcThreads), lds, st, d_img, C, d_feat, F,
                      d_a, d_b, d_centers, k, d_label, n_pix, M, part);
   MW_LAUNCH_CHECK();
-  hipLaunchKernelGGL(domain_sse_reduce, dim3((M + 255) / 256), dim3(256), 0, st, part, G, M, d_out);
+  hipLaunchKernelGGL(domain_sse_reduce, dim3(M), dim3(256), 0, st, part, G, M, d_out);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
