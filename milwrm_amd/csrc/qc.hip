@@ -13,8 +13,8 @@
 // Layout: a block of 256 threads is split into floor(256/F) groups of F lanes;
 // lane f of a group owns feature f, so a wave reads whole pixels (F contiguous
 // floats for identity features) and every lane keeps its own per-domain
-// column of fp64 accumulators in LDS (no atomics, no bank conflicts); four
-// pixels' loads are issued before their updates.  Per-block partials go to a
+// column of fp64 accumulators in LDS (no atomics, no bank conflicts); eight
+// pixels' loads are issued before their updates (kQcUnroll = 8).  Per-block partials go to a
 // workspace and a second kernel folds them in a fixed order (deterministic).  HBM-bound: n_pix * (C*4 + 1) bytes.
 #include "common.h"
 
@@ -23,6 +23,7 @@ namespace mw {
 constexpr int kQcThreads = 256;
 constexpr int kQcMaxK = 20;  // LDS <= 20*256*8 + 2*256*8 + 20*256*4 (F = 1) = 64 KiB, the default limit
 constexpr int kQcMaxBlocks = 2048;
+constexpr int kQcUnroll = 8;
 
 __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
     const float* __restrict__ img, int C, const int32_t* __restrict__ feat, int F,
@@ -55,17 +56,17 @@ __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
       }
     };
     int64_t p = (int64_t)blockIdx.x * groups + g;
-    // four pixels' loads in flight before their (LDS read-modify-write) updates
-    for (; p + 3 * step < n_pix; p += 4 * step) {
-      float v[4];
-      int l[4];
+    // kQcUnroll pixels' loads in flight before their (LDS read-modify-write) updates
+    for (; p + (kQcUnroll - 1) * step < n_pix; p += kQcUnroll * step) {
+      float v[kQcUnroll];
+      int l[kQcUnroll];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kQcUnroll; ++u) {
         v[u] = img[(p + u * step) * C + ch];
         l[u] = label[p + u * step];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) add(v[u], l[u]);
+      for (int u = 0; u < kQcUnroll; ++u) add(v[u], l[u]);
     }
     for (; p < n_pix; p += step) add(img[p * C + ch], label[p]);
   }
