@@ -23,8 +23,8 @@
  *                                                          MxIF.py:484,490
  *   mw_col_stats_finalize StandardScaler.fit               MILWRM.py:1742-1745
  *   mw_kpp_*           sklearn _kmeans_plusplus            _kmeans.py:174-272
- *   mw_lloyd_step,
- *   mw_lloyd_reduce    sklearn lloyd_iter_chunked_dense    _k_means_lloyd.pyx:23-218
+ *   mw_lloyd_pass      sklearn lloyd_iter_chunked_dense    _k_means_lloyd.pyx:23-218
+ *                      (+ _inertia_dense                   _k_means_common.pyx:94-124)
  *   mw_farthest        sklearn _relocate_empty_clusters_dense _k_means_common.pyx:181-226
  *   mw_assign_conf     KMeans.predict + estimate_confidence_score_mxif
  *                                                          MILWRM.py:237-277, 389-450
@@ -200,32 +200,55 @@ int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu,
                  const double* d_inv, int c, int best, const float* d_rows, int T,
                  void* d_ws, void* stream);
 
-/* ---- Lloyd E(+M) step (sklearn _k_means_lloyd.pyx:23-218) -------------------
- * Rows x' = x*scale_a[f] + scale_b[f] (fp32 affine, the folded StandardScaler).
- * Labels argmin of the direct squared distance, lowest index on ties.
- * mode 0: E+M (labels updated, changed count, per-cluster sums/counts)
- * mode 1: E only + inertia (labels updated, sum of min distances)
- * mode 2: inertia of the given labels only (fp64 distances)
- * Per-block partial records [sums k*F | counts k | changed | inertia] go to
- * d_ws; mw_lloyd_reduce folds them (fixed order) into d_out (fp64). */
+/* ---- Lloyd iteration (sklearn lloyd_iter_chunked_dense, _k_means_lloyd.pyx:23-218;
+ *      _inertia_dense, _k_means_common.pyx:94-124) -----------------------------
+ * One pass over S rows for n independent fits (n = 1 for KMeans.fit, all k of
+ * the find_optimal_k sweep, MILWRM.py:29-90, batched).  Rows x' = x*a[f] +
+ * b[f] (fp32, the folded StandardScaler); labels = argmin of the direct
+ * squared distance, lowest index on ties.  Per fit the caller owns:
+ *   centers   k x F fp32 (scaled space)
+ *   labels    S uint8 (255 = none yet; k <= 64)
+ *   ub, lb    S fp32 distance bounds (mode 0; contents ignored where label = 255)
+ *   drift     k fp32 |c_j - c_j(previous pass)|, rounded up (0 on the first pass)
+ *   half_sep  k fp32 0.5 * min_{i != j} |c_i - c_j|, rounded down (+inf for k = 1)
+ *   drift_max max_j drift[j]
+ *   ws        mw_lloyd_ws_bytes(S, k, F) bytes of per-block records
+ *   out       mw_lloyd_rec_len(k, F) fp64, the fixed-order fold of the records:
+ *             [dQ_hi k*F | dQ_lo k*F | dcount k | changed | recomputed | in_hi | in_lo]
+ * mode 0: E-step (rows whose bounds prove the label skip the distances) and
+ *         the M-step change of the per-cluster sums: every raw value rounds
+ *         once to q = rint(x * 2^qexp[f]) (|q| < 2^41) and a relabelled row
+ *         moves its q from the old cluster to the new one; dQ = dQ_hi * 2^32 +
+ *         dQ_lo (exact integers), dcount the change of the cluster sizes.
+ * mode 1: full E-step (labels updated) and inertia = (in_hi * 2^32 + in_lo) *
+ *         2^-inertia_exp of the new labels (each distance rounded once to that
+ *         fixed point);  mode 2: inertia of the given labels.
+ * Every sum is an integer sum: identical for any row order or sharding.
+ * `kind` (mode 0): 0 = first pass (every label 255: sums of all rows on the
+ * fp64 matrix cores), 1 = stream every row, the bounds skip the E-step per
+ * row (most rows undecided), 2 = stream the row state only and read just the
+ * undecided rows (few undecided).  Same results for any kind.
+ * k <= 64, F <= 64, n <= 24.  h_fits is a host array. */
+typedef struct mw_lloyd_fit {
+  const float* centers;
+  const float* drift;
+  const float* half_sep;
+  uint8_t* labels;
+  float* ub;
+  float* lb;
+  void* ws;
+  double* out;
+  int k;
+  float drift_max;
+  int inertia_exp;  /* modes 1 / 2: inertia fixed point 2^-inertia_exp */
+} mw_lloyd_fit;
+int mw_lloyd_rec_len(int k, int F);
 size_t mw_lloyd_ws_bytes(int64_t S, int k, int F);
-int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a,
-                  const float* d_b, const float* d_centers, int k,
-                  uint8_t* d_labels, int mode, void* d_ws, void* stream);
-int mw_lloyd_reduce(const void* d_ws, int64_t S, int k, int F, double* d_out,
-                    void* stream);
-/* n independent fits over the same rows in one pass (the k sweep of
- * find_optimal_k, MILWRM.py:29-90): fit g has k = h_k[g] centers
- * (d_centers[g], fp32 k x F), labels h_labels[g] and workspace h_ws[g]
- * (mw_lloyd_ws_bytes(S, h_k[g], F)); the step is followed by the
- * mw_lloyd_reduce of every fit into h_out[g].  Results are bitwise those of n
- * separate mw_lloyd_step + mw_lloyd_reduce calls.  n <= 24; all fits of one
- * call in the same class k <= 16 / 17..32 / 33..64. Host arrays of device
- * pointers. */
-int mw_lloyd_step_multi(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
-                        int n, const float* const* h_centers, const int* h_k,
-                        uint8_t* const* h_labels, int mode, void* const* h_ws,
-                        double* const* h_out, void* stream);
+int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
+                  const int32_t* d_qexp, int n, const mw_lloyd_fit* h_fits, int mode, int kind,
+                  void* stream);
+/* per-column max |x| of S x F fp32 rows (F <= 256), fp32 out */
+int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream);
 
 /* ---- empty-cluster relocation support (_k_means_common.pyx:181-226) ---------
  * fp64 distance of every row to centers[labels]; returns the n largest

@@ -60,9 +60,9 @@ _PROTOS = {
     "mw_kpp_search": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "mw_kpp_trial": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_lloyd_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
-    "mw_lloyd_step_multi": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
-    "mw_lloyd_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),
-    "mw_lloyd_reduce": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "mw_lloyd_rec_len": (c_i32, [c_i32, c_i32]),
+    "mw_lloyd_pass": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp]),
+    "mw_col_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_farthest_ws_bytes": (c_sz, [c_i64]),
     "mw_farthest": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_ws_bytes": (c_sz, [c_i64, c_i32]),
@@ -81,6 +81,13 @@ _PROTOS = {
 }
 
 EXPORTED = tuple(_PROTOS)
+
+
+class LloydFit(C.Structure):
+    """``mw_lloyd_fit`` (include/milwrm_amd.h)."""
+    _fields_ = [("centers", c_vp), ("drift", c_vp), ("half_sep", c_vp), ("labels", c_vp),
+                ("ub", c_vp), ("lb", c_vp), ("ws", c_vp), ("out", c_vp), ("k", c_i32),
+                ("drift_max", c_f32), ("inertia_exp", c_i32)]
 
 
 class NativeError(RuntimeError):

@@ -3,7 +3,7 @@
 // MxIF.py:416-455 / 375-394; scipy gaussian_filter mode='nearest', truncate=4)
 // — the fast path for radius 1..8 (sigma <= 2.1) and even C <= 64.
 //
-// A workgroup owns a band of BW = 16*BT output columns x kBlurBH output rows
+// A workgroup owns a band of BW = 16*BT output columns x bh output rows (BlurGrid)
 // and all channels; wave (tx, ct) owns the 16-column x 16-channel output tile
 // (BT x ceil(C/16) waves).  Rows stream top to bottom through three stages:
 //   1. input: the halo'd row segment (BW + 2r columns x C channels, one
@@ -157,11 +157,40 @@ struct BlurMfmaCfg {
   static constexpr size_t lds_bytes() { return FIXED + (size_t)D * SLOT; }
 };
 
+// Band grid: nbx column bands x nby row bands of bh rows, one workgroup each,
+// launched as a 1-D grid (column band fastest).  Measured at 10k^2 x 30
+// (tools/blur_bench.py): 256-row bands 5.29 ms; 128 / 385 / 512 / 770 rows
+// 5.36 / 5.46 / 5.35 / 5.50 ms (fewer, taller bands do not pay despite their
+// smaller halo share); dealing adjacent bands to one XCD (xcd = 1: block b
+// takes logical tile (b % 8) * (tiles / 8) + b / 8) 5.49 ms.  MW_BLUR_BH and
+// MW_BLUR_XCD override both for tuning.
+struct BlurGrid {
+  int bh, nbx, ntiles, xcd;
+  __device__ __forceinline__ void tile(int b, int G, int& bx, int& by) const {
+    const int x = b & 7, j = b >> 3, q = G >> 3, rem = G & 7;
+    const int t = xcd ? x * q + (x < rem ? x : rem) + j : b;
+    by = t / nbx;
+    bx = t - by * nbx;
+  }
+};
+
+static inline BlurGrid blur_grid(int H, int nbx) {
+  BlurGrid g;
+  g.nbx = nbx;
+  g.bh = kBlurBH;
+  g.xcd = 0;
+  if (const char* e = getenv("MW_BLUR_BH")) g.bh = atoi(e) >= 16 ? atoi(e) : kBlurBH;
+  if (const char* e = getenv("MW_BLUR_XCD")) g.xcd = atoi(e);
+  g.ntiles = nbx * ((H + g.bh - 1) / g.bh);
+  return g;
+}
+
 template <typename T, int R, int CT, int BT, bool LOGN, int EPI>
 __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_mfma_kernel(const T* __restrict__ in, int H, int W,
                                                                  int C, const float* __restrict__ inv_mean,
                                                                  float pseudo, BlurTaps taps,
-                                                                 float* __restrict__ out, BlurEpi ep) {
+                                                                 float* __restrict__ out, BlurEpi ep,
+                                                                 BlurGrid bg) {
   using K = BlurMfmaCfg<T, R, CT, BT, EPI>;
   constexpr int NS = K::NS, KS = kEpiKS;
   constexpr int NR = K::NR, BW = K::BW, NPX = K::NPX, PS = K::PS, NK = K::NK, NT = K::NT;
@@ -187,9 +216,11 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
   const int lane = t & 63;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int tx = wv % BT, ct = wv / BT;
-  const int x0 = blockIdx.x * BW;
-  const int y0 = blockIdx.y * kBlurBH;
-  const int y1 = min(H, y0 + kBlurBH);
+  int bx, by;
+  bg.tile(blockIdx.x, gridDim.x, bx, by);
+  const int x0 = bx * BW;
+  const int y0 = by * bg.bh;
+  const int y1 = min(H, y0 + bg.bh);
   const int nrows = (y1 - y0) + 2 * R;
   const int bw = min(BW, W - x0);
   // clamped input column range [xa, xb) and its position in the halo'd row
@@ -529,13 +560,17 @@ static int launch_blur_mfma_rc(const T* in, int H, int W, int C, const float* in
   {
     const size_t lds = K::lds_bytes();
     if (lds > 160 * 1024 || K::D < 4) return MW_EUNSUPPORTED;
-    dim3 grid((W + K::BW - 1) / K::BW, (H + kBlurBH - 1) / kBlurBH);
+    const int nbx = (W + K::BW - 1) / K::BW;
     if (inv_mean) {
-      hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, true, EPI>), grid, dim3(K::NT), lds, st, in, H,
-                         W, C, inv_mean, p, taps, out, ep);
+      auto kern = blur_mfma_kernel<T, R, CT, BT, true, EPI>;
+      const BlurGrid bg = blur_grid(H, nbx);
+      hipLaunchKernelGGL(kern, dim3(bg.ntiles), dim3(K::NT), lds, st, in, H, W, C, inv_mean, p, taps, out,
+                         ep, bg);
     } else if constexpr (EPI == kEpiStore) {
-      hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, false, EPI>), grid, dim3(K::NT), lds, st, in, H,
-                         W, C, inv_mean, p, taps, out, ep);
+      auto kern = blur_mfma_kernel<T, R, CT, BT, false, EPI>;
+      const BlurGrid bg = blur_grid(H, nbx);
+      hipLaunchKernelGGL(kern, dim3(bg.ntiles), dim3(K::NT), lds, st, in, H, W, C, inv_mean, p, taps, out,
+                         ep, bg);
     } else {
       return MW_EUNSUPPORTED;  // the fused epilogues follow a log-normalise
     }

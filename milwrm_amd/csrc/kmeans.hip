@@ -1,8 +1,7 @@
 // k-means kernels of the MILWRM hot path on MI355X (gfx950, wave64).
 //
 //   kpp_*        sklearn _kmeans_plusplus            _kmeans.py:174-272
-//   lloyd_step   lloyd_iter_chunked_dense            _k_means_lloyd.pyx:23-218
-//                (+ _inertia_dense, _k_means_common.pyx:94-124)
+//   (the Lloyd iteration itself is lloyd.hip)
 //   farthest     _relocate_empty_clusters_dense      _k_means_common.pyx:181-226
 //   assign_conf  KMeans.predict + estimate_confidence_score_mxif
 //                                                    MILWRM.py:237-277, 389-450
@@ -15,84 +14,16 @@
 #include <math.h>
 #include <stdlib.h>
 
-#include "common.h"
+#include "kmeans_common.h"
 
 namespace mw {
 
-#ifndef MW_LLOYD_WPS
-// waves per SIMD the Lloyd pass is compiled for: 3 for the F <= 32, k <= 16
-// instance (168 VGPRs, no spill; 6 % faster than 2 waves at 200 VGPRs),
-// 1 (no bound) for the larger tiles, which would spill
-#define MW_LLOYD_WPS ((FMAX <= 32 && MB == 1) ? 3 : 1)
-#endif
 #ifndef MW_ASSIGN_WPS
 #define MW_ASSIGN_WPS 1
 #endif
 #ifndef MW_KPP_WPS
 #define MW_KPP_WPS 1
 #endif
-
-constexpr int kT = 256;          // rows per tile = threads per block
-constexpr int kMaxG = 1024;
-
-static inline int kmax_grid() {
-  static int g = [] {
-    const char* e = getenv("MW_KBLOCKS");  // tuning override (<= kMaxG)
-    const int v = e ? atoi(e) : 0;
-    return (v >= 1 && v <= kMaxG) ? v : kMaxG;
-  }();
-  return g;
-}
-static inline int kblocks(int64_t n) {
-  int64_t tiles = (n + kT - 1) / kT;
-  if (tiles < 1) tiles = 1;
-  const int gm = kmax_grid();
-  return (int)(tiles < gm ? tiles : gm);
-}
-static inline int64_t krows(int64_t n) {
-  int64_t tiles = (n + kT - 1) / kT;
-  int g = kblocks(n);
-  return ((tiles + g - 1) / g) * kT;
-}
-
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef float f4v __attribute__((ext_vector_type(4)));
-__host__ __device__ constexpr int kpad4(int k) { return (k + 3) & ~3; }
-
-// ---- wave tiles: 64 consecutive rows of F floats (64*F floats, float4-aligned
-// because tile starts are multiples of 64 rows).  Each lane fetches NV =
-// FMAX/4 float4 with clamped, unconditional loads (guide §5.4c) and stores all
-// of them to the wave's LDS tile of 64*FMAX floats: floats past 64*F are the
-// following rows' data, read by the E-step only for padded features whose scale
-// is exactly 0.  Floats past the array's last whole float4 are patched with
-// scalar loads in the final tile only.
-__device__ __forceinline__ void wt_tail(int nfl, int64_t e0, int64_t n4, const float* __restrict__ X,
-                                        int64_t total, float* s, int lane) {
-  if (e0 + nfl > n4 * 4) {  // wave-uniform
-    for (int e = lane; e < nfl; e += 64) {
-      const int64_t ge = e0 + e;
-      if (ge >= n4 * 4 && ge < total) s[e] = X[ge];
-    }
-  }
-}
-
-// ---- wave-tile streaming with buffer loads: the resource covers a block's
-// rows from its first row to the end of the array (32-bit block-relative
-// offsets, hardware range check), the tile offset is a scalar (tile index is
-// wave-uniform) and the per-lane offsets are constants, so a tile fetch costs
-// no VALU.  Loads past the end return 0; stores past the range are dropped.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t nbytes) {
-  const uint64_t n = nbytes < 0 ? 0 : (uint64_t)nbytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
-                                           (int)(uint32_t)(n < 0xFFFFFFFFull ? n : 0xFFFFFFFFull),
-                                           0x00020000);
-}
-template <int NV>
-__device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t rs, int soff, int lane, f4v (&v)[NV]) {
-#pragma unroll
-  for (int i = 0; i < NV; ++i)
-    v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + i * 1024, soff, 0));
-}
 
 constexpr int kKppTab = 64 * 9;  // doubles: k-means++ candidate table inv[64] | b[64][8]
 
@@ -373,436 +304,9 @@ __global__ void __launch_bounds__(256, MW_KPP_WPS) kpp_dist_kernel(
   }
 }
 
-// ---- E-step center stream, written as inline asm so that the schedule is
-// the one below (hipcc otherwise hoists every center read of the block, 128+
-// VGPRs, and serialises the four distance chains).  hipcc does not count asm
-// memory operations in its s_waitcnt bookkeeping, so the stream waits itself
-// with counted lgkmcnt: LDS returns in order, and any LDS op the compiler
-// places in between only makes a counted wait stricter.
-template <int OFF>
-__device__ __forceinline__ f2v ds_read8(uint32_t addr) {
-  f2v r;
-  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
-  return r;
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait4(f2v (&c)[4]) {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
-  asm volatile("" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]));  // uses stay below the wait
-}
-// acc[q] += (x - c[q])^2 for four centers, packed over a feature pair: the four
-// subtractions then the four FMAs (no dependent pair back to back)
-__device__ __forceinline__ void dist4(f2v x, const f2v (&c)[4], f2v (&acc)[4]) {
-  f2v d0, d1, d2, d3;
-  asm volatile(
-      "v_pk_add_f32 %0, %8, %9 neg_lo:[0,1] neg_hi:[0,1]\n\t"
-      "v_pk_add_f32 %1, %8, %10 neg_lo:[0,1] neg_hi:[0,1]\n\t"
-      "v_pk_add_f32 %2, %8, %11 neg_lo:[0,1] neg_hi:[0,1]\n\t"
-      "v_pk_add_f32 %3, %8, %12 neg_lo:[0,1] neg_hi:[0,1]\n\t"
-      "v_pk_fma_f32 %4, %0, %0, %4\n\t"
-      "v_pk_fma_f32 %5, %1, %1, %5\n\t"
-      "v_pk_fma_f32 %6, %2, %2, %6\n\t"
-      "v_pk_fma_f32 %7, %3, %3, %7"
-      : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]),
-        "+v"(acc[3])
-      : "v"(x), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]));
-}
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
-}
-
-// Nearest center (strict '<': the lowest index wins exact ties, as the
-// reference's argmin) and, with TOP2, the second smallest distance.  Squared
-// distances of the scaled row x2 to every center; the centers sit in LDS
-// pair-major with a fixed center stride KS (cT[p * KS + j] = features 2p, 2p+1
-// of center j; zero past k), so each read is a broadcast ds_read_b64 at an
-// immediate offset.  Four centers per pass keep four independent packed-FMA
-// chains; center pairs stream kAhead pairs ahead of their FMAs.  Each center's
-// chain (even features in .x, odd in .y, then .x + .y) is the same fp32
-// operation sequence as a one-center loop, so the result does not depend on
-// the blocking.
-#ifndef MW_KAHEAD
-#define MW_KAHEAD 1
-#endif
-constexpr int kAhead = MW_KAHEAD;  // center pairs in flight ahead of their FMAs
-template <int NP, int KS, int P>
-__device__ __forceinline__ void nc_read(uint32_t base, f2v (&c)[4]) {
-  c[0] = ds_read8<P * KS * 8>(base);
-  c[1] = ds_read8<P * KS * 8 + 8>(base);
-  c[2] = ds_read8<P * KS * 8 + 16>(base);
-  c[3] = ds_read8<P * KS * 8 + 24>(base);
-}
-template <int NP, int KS, int P>
-__device__ __forceinline__ void nc_pairs(uint32_t base, const f2v* x2, f2v (*c)[4], f2v (&acc)[4]) {
-  if constexpr (P < NP) {
-    if constexpr (P + kAhead < NP) nc_read<NP, KS, P + kAhead>(base, c[(P + kAhead) % (kAhead + 1)]);
-    constexpr int after = 4 * ((P + kAhead < NP) ? kAhead : (NP - 1 - P));
-    lgkm_wait4<after>(c[P % (kAhead + 1)]);
-    dist4(x2[P], c[P % (kAhead + 1)], acc);
-    nc_pairs<NP, KS, P + 1>(base, x2, c, acc);
-  }
-}
-template <int NP, int KS, int P>
-__device__ __forceinline__ void nc_prologue(uint32_t base, f2v (*c)[4]) {
-  if constexpr (P < kAhead && P < NP) {
-    nc_read<NP, KS, P>(base, c[P]);
-    nc_prologue<NP, KS, P + 1>(base, c);
-  }
-}
-template <int FMAX, int KS, bool TOP2>
-__device__ __forceinline__ void nearest_centers(const f2v (&x2)[FMAX / 2], const f2v* cT, int k,
-                                                int& lab, float& m1, float& m2) {
-  constexpr int NP = FMAX / 2;
-  const uint32_t a0 = lds_addr(cT);
-  lab = 0;
-  m1 = 0.f;
-  m2 = __builtin_inff();
-  for (int j0 = 0; j0 < k; j0 += 4) {
-    const uint32_t base = a0 + (uint32_t)j0 * 8u;
-    f2v c[kAhead + 1][4];  // register ring of center pairs in flight
-    f2v acc[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = f2v{0.f, 0.f};
-    nc_prologue<NP, KS, 0>(base, c);
-    nc_pairs<NP, KS, 0>(base, x2, c, acc);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = j0 + q;
-      if (j < k) {
-        const float dd = acc[q].x + acc[q].y;
-        if (TOP2) {
-          if (j == 0) { m1 = dd; lab = 0; }
-          else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
-          else if (dd < m2) { m2 = dd; }
-        } else if (j == 0 || dd < m1) {
-          m1 = dd;
-          lab = j;
-        }
-      }
-    }
-  }
-}
-
-// centers (k x F row-major, global) -> pair-major LDS image cT (see above)
-template <int FMAX, int KS>
-__device__ __forceinline__ void load_centers_T(const float* __restrict__ gc, int k, int F, f2v* cT) {
-  for (int q = threadIdx.x; q < (FMAX / 2) * KS; q += blockDim.x) {
-    const int p = q / KS, j = q - p * KS;
-    const int f0 = 2 * p, f1 = 2 * p + 1;
-    cT[q] = f2v{(j < k && f0 < F) ? gc[j * F + f0] : 0.f, (j < k && f1 < F) ? gc[j * F + f1] : 0.f};
-  }
-}
-
-// the lane's row of a 64-row LDS tile (row stride F floats), scaled x*a + b;
-// features past F scale to exactly 0 (a = b = 0 there)
-template <int FMAX>
-__device__ __forceinline__ void load_scaled_row(const float* s_tile, int lane, int F, const float* sa_,
-                                                const float* sb_, f2v (&x2)[FMAX / 2]) {
-  int z = 0;
-  asm volatile("" : "+s"(z));  // re-read the scaler from LDS each tile (no pinned registers)
-  const f2v* sa = reinterpret_cast<const f2v*>(sa_) + z;
-  const f2v* sb = reinterpret_cast<const f2v*>(sb_) + z;
-  const float* xs = s_tile + lane * F;
-  if ((F & 1) == 0) {  // 8-byte aligned rows: ds_read_b64 pairs
-    const f2v* xp = reinterpret_cast<const f2v*>(__builtin_assume_aligned(xs, 8));
-#pragma unroll
-    for (int p = 0; p < FMAX / 2; ++p) {
-      x2[p] = __builtin_elementwise_fma(xp[p], sa[p], sb[p]);
-      // groups of 4 pairs: keeps the scaler reads from all being hoisted
-      // (3 x 32 transient VGPRs)
-      if ((p & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-#pragma unroll
-    for (int p = 0; p < FMAX / 2; ++p)
-      x2[p] = __builtin_elementwise_fma(f2v{xs[2 * p], xs[2 * p + 1]}, sa[p], sb[p]);
-  }
-}
-
-// ================================================================== Lloyd
-// Per-block record: [sums k*F | counts k | changed | inertia] (fp64).
-__host__ __device__ inline int lloyd_rec(int k, int F) { return k * F + k + 2; }
-
-
-// bytes of one wave's LDS region: row tile [64*FMAX] | labels [64]
-__host__ __device__ inline size_t lloyd_wave_bytes(int FMAX) { return (size_t)64 * FMAX * 4 + 64 * 4; }
-// pair-major center image (FMAX/2 x kpad4(k) float pairs)
-__host__ __device__ inline size_t cent_t_bytes(int KS, int FMAX) {
-  return (size_t)(FMAX / 2) * KS * 8;
-}
-
-// One Lloyd pass (lloyd_iter_chunked_dense, _k_means_lloyd.pyx:23-218):
-//   MODE 0: assign + relabel + per-label sums/counts (M-step partials)
-//   MODE 1: assign + relabel + inertia of the new labels
-//   MODE 2: inertia of the given labels (_inertia_dense, _k_means_common.pyx:94-124)
-// Every wave streams its own 64-row tiles (tile w, w+nw, ... of the block's
-// row range) with the next tile's loads in flight during the current tile's
-// work; no block barrier until the final combine.
-//   E-step: lane = row, scaled row x' = x*a + b (fp32), squared distances by
-//           packed-FMA chains, four centers per pass (nearest_centers), strict
-//           argmin.
-//   M-step: per-label sums of the RAW rows as a one-hot GEMM on the f32 MFMA
-//           (v_mfma_f32_16x16x4_f32: A[label][row] = onehot, B[row][feature] =
-//           x; bit-exact fp32 FMA chain in row order), 16 labels x 16 features
-//           per accumulator, flushed into fp64 registers after every 64-row
-//           tile.  The LDS operands of 8 k-steps are read in one batch before
-//           their MFMAs.  The record holds a*sum(x) + b*count = sum of scaled
-//           rows.
-template <int FMAX, int MB, int MODE>
-__device__ __forceinline__ void lloyd_body(const float* __restrict__ X, int64_t S, int F,
-                                           const float* __restrict__ ga,
-                                           const float* __restrict__ gb,
-                                           const float* __restrict__ gc, int k,
-                                           uint8_t* __restrict__ labels,
-                                           int64_t R, double* __restrict__ rec, const int blk) {
-  constexpr int NV = FMAX / 4;                   // float4 per lane per tile
-  constexpr int NB = FMAX <= 16 ? 1 : FMAX / 16;  // 16-feature MFMA column blocks
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ __attribute__((aligned(16))) float s_a[FMAX], s_b[FMAX];
-  __shared__ long long s_wcnt[4 * 64];
-  __shared__ double s_red[4];
-  const int t = threadIdx.x, lane = t & 63, nw = blockDim.x >> 6;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  f2v* s_cT = reinterpret_cast<f2v*>(smem);
-  const size_t cent_bytes = cent_t_bytes(64, FMAX);
-  double* s_blk = reinterpret_cast<double*>(smem + cent_bytes);  // k * F block sums
-  const size_t blk_bytes = ((size_t)k * F * 8 + 15) & ~(size_t)15;
-  float* s_tile = reinterpret_cast<float*>(smem + cent_bytes + blk_bytes + (size_t)wid * lloyd_wave_bytes(FMAX));
-  int* s_lab = reinterpret_cast<int*>(s_tile + 64 * FMAX);
-
-  load_centers_T<FMAX, 64>(gc, k, F, s_cT);
-  for (int f = t; f < FMAX; f += blockDim.x) {
-    s_a[f] = f < F ? ga[f] : 0.f;  // padded features scale to exactly 0
-    s_b[f] = f < F ? gb[f] : 0.f;
-  }
-  if (MODE == 0)
-    for (int q = t; q < k * F; q += blockDim.x) s_blk[q] = 0.0;
-  __syncthreads();
-
-  const int64_t lo = (int64_t)blk * R, hi = min(S, lo + R);
-  const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
-  const int64_t total = S * (int64_t)F, n4 = total >> 2;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + lo * F, (S - lo) * F * 4);
-  const __amdgpu_buffer_rsrc_t rl = make_rsrc(labels + lo, hi - lo);
-  const int tile_bytes = 64 * F * 4;
-  const int kk = lane >> 4, jj = lane & 15;  // MFMA operand lane map
-  double inert = 0.0;
-  long long changed = 0, cnt = 0;
-  double acc64[MB][NB][4];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc64[mb][nb][r] = 0.0;
-
-  f4v v[NV];
-  int old_next = 0;
-  // fetch tile `tt` (clamped to the last tile: a harmless re-read)
-  auto fetch = [&](int tt) {
-    tt = tt < ntile ? tt : ntile - 1;
-    old_next = __builtin_amdgcn_raw_buffer_load_b8(rl, lane, tt * 64, 0);
-    tile_load<NV>(rx, tt * tile_bytes, lane, v);
-  };
-  int tc = wid;
-  if (tc < ntile) fetch(tc);
-  for (; tc < ntile; tc += nw) {
-    const int64_t r0 = lo + (int64_t)tc * 64;
-    const int nrow = (int)min((int64_t)64, hi - r0);
-    {
-      f4v* s4 = reinterpret_cast<f4v*>(s_tile);
-#pragma unroll
-      for (int i = 0; i < NV; ++i) s4[lane + i * 64] = v[i];
-    }
-    wt_tail(nrow * F, r0 * F, n4, X, total, s_tile, lane);
-    const int old = old_next;
-    fetch(tc + nw);  // the next tile's loads stay in flight during this tile
-    const bool valid = lane < nrow;
-    // ---- E-step ----
-    f2v x2[FMAX / 2];
-    load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
-    int lab;
-    float best;
-    if (MODE == 2) {
-      lab = old;
-      f2v acc = f2v{0.f, 0.f};
-#pragma unroll
-      for (int p = 0; p < FMAX / 2; ++p) {
-        const f2v d = x2[p] - s_cT[p * 64 + lab];
-        acc = __builtin_elementwise_fma(d, d, acc);
-      }
-      best = acc.x + acc.y;
-    } else {
-      float m2u;
-#ifdef MW_X_NOE
-      lab = old; best = x2[0].x;
-#else
-      nearest_centers<FMAX, 64, false>(x2, s_cT, k, lab, best, m2u);
-#endif
-      changed += (valid && lab != old) ? 1 : 0;
-      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)lab, rl, lane, tc * 64, 0);
-    }
-    if (MODE >= 1 && valid) inert += (double)best;
-    if (MODE == 0) {
-      // ---- M-step partials ----
-      s_lab[lane] = valid ? lab : -1;
-      for (int j = 0; j < k; ++j) {
-        const unsigned long long m = __ballot(valid && lab == j);
-        if (lane == j) cnt += __popcll(m);
-      }
-      f4v d[MB][NB];
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) d[mb][nb] = f4v{0.f, 0.f, 0.f, 0.f};
-      const float* xrow = s_tile + kk * F;  // row 4*st + kk at + 4*st*F
-      int bcol[NB];
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) bcol[nb] = min(16 * nb + jj, F - 1);  // cols >= F never read back
-#ifndef MW_X_NOM  // (ablation builds only: no M-step MFMAs)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {  // two batches of 8 k-steps (4 rows each)
-        int Lr[8];
-        float xb[8][NB];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int st = 8 * h + u;
-          Lr[u] = s_lab[4 * st + kk];
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) xb[u][nb] = xrow[4 * st * F + bcol[nb]];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-#pragma unroll
-          for (int mb = 0; mb < MB; ++mb) {
-            const float a = (Lr[u] == 16 * mb + jj) ? 1.f : 0.f;
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-              d[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xb[u][nb], d[mb][nb], 0, 0, 0);
-          }
-        }
-      }
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc64[mb][nb][r] += (double)d[mb][nb][r];
-#endif
-    }
-  }
-  // ---- block record (fixed combine order: waves in index order) ----
-  s_wcnt[wid * 64 + lane] = cnt;
-  const double ch = block_sum((double)changed, s_red);
-  const double in = block_sum(inert, s_red);
-  const int rlen = lloyd_rec(k, F);
-  double* out = rec + (size_t)blk * rlen;
-  if (MODE == 0) {
-    for (int w = 0; w < nw; ++w) {
-      if (wid == w) {
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int i = 16 * mb + 4 * kk + r, f = 16 * nb + jj;  // C/D lane map
-              if (i < k && f < F) s_blk[i * F + f] += acc64[mb][nb][r];
-            }
-      }
-      __syncthreads();
-    }
-    for (int q = t; q < k * F; q += blockDim.x) {
-      const int j = q / F, f = q - j * F;
-      long long n = 0;
-      for (int w = 0; w < nw; ++w) n += s_wcnt[w * 64 + j];
-      out[q] = (double)s_a[f] * s_blk[q] + (double)s_b[f] * (double)n;
-    }
-    for (int j = t; j < k; j += blockDim.x) {
-      long long n = 0;
-      for (int w = 0; w < nw; ++w) n += s_wcnt[w * 64 + j];
-      out[k * F + j] = (double)n;
-    }
-  } else {
-    for (int q = t; q < k * F + k; q += blockDim.x) out[q] = 0.0;
-  }
-  if (t == 0) {
-    out[k * F + k] = ch;
-    out[k * F + k + 1] = in;
-  }
-}
-
-template <int FMAX, int MB, int MODE>
-__global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_kernel(const float* __restrict__ X, int64_t S, int F,
-                                                    const float* __restrict__ ga,
-                                                    const float* __restrict__ gb,
-                                                    const float* __restrict__ gc, int k,
-                                                    uint8_t* __restrict__ labels,
-                                                    int64_t R, double* __restrict__ rec) {
-  lloyd_body<FMAX, MB, MODE>(X, S, F, ga, gb, gc, k, labels, R, rec, blockIdx.x);
-}
-
-// Several independent fits over the same rows in one launch (the
-// find_optimal_k sweep, MILWRM.py:29-90): block i runs fit i % n of row block
-// i / n, so the n blocks that read one row block are dispatched together and
-// all but the first find those rows in the on-die caches instead of HBM.
-// Per fit the arithmetic (row -> block map, per-block records, combine order)
-// is the single-fit kernel's: results are bitwise those of separate fits.
-constexpr int kMaxFits = 24;
-struct LloydFits {
-  const float* centers[kMaxFits];
-  uint8_t* labels[kMaxFits];
-  double* rec[kMaxFits];
-  double* out[kMaxFits];
-  int k[kMaxFits];
-};
-template <int FMAX, int MB, int MODE>
-__global__ void __launch_bounds__(256, MW_LLOYD_WPS) lloyd_multi_kernel(const float* __restrict__ X, int64_t S,
-                                                          int F, const float* __restrict__ ga,
-                                                          const float* __restrict__ gb,
-                                                          const LloydFits fits, int n, int64_t R) {
-  const int g = blockIdx.x % n, blk = blockIdx.x / n;
-  lloyd_body<FMAX, MB, MODE>(X, S, F, ga, gb, fits.centers[g], fits.k[g], fits.labels[g], R,
-                             fits.rec[g], blk);
-}
-
-// fixed-order sum of G per-block records: thread (q, part) sums blocks
-// b = part, part+8, ... with 8 independent partial sums, then parts combine
-// in order.
-__device__ __forceinline__ void lloyd_reduce_body(const double* __restrict__ rec, int G, int rl,
-                                                  double* __restrict__ out) {
-  __shared__ double s[8][33];
-  const int lane = threadIdx.x & 31, part = threadIdx.x >> 5;  // 32 columns x 8 parts
-  const int q = blockIdx.x * 32 + lane;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  if (q < rl) {
-    int b = part;
-    for (; b + 24 < G; b += 32) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] += rec[(size_t)(b + 8 * u) * rl + q];
-    }
-    for (; b < G; b += 8) acc[0] += rec[(size_t)b * rl + q];
-  }
-  s[part][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  __syncthreads();
-  if (part == 0 && q < rl) {
-    double t = 0.0;
-#pragma unroll
-    for (int p2 = 0; p2 < 8; ++p2) t += s[p2][lane];
-    out[q] = t;
-  }
-}
-
-__global__ void __launch_bounds__(256) lloyd_reduce_kernel(const double* __restrict__ rec, int G,
+__global__ void __launch_bounds__(256) rec_reduce_kernel(const double* __restrict__ rec, int G,
                                                            int rl, double* __restrict__ out) {
-  lloyd_reduce_body(rec, G, rl, out);
-}
-// one fit per blockIdx.y (records of lloyd_multi_kernel)
-__global__ void __launch_bounds__(256) lloyd_reduce_multi_kernel(const LloydFits fits, int G, int F) {
-  const int g = blockIdx.y, k = fits.k[g];
-  const int rl = lloyd_rec(k, F);
-  if ((int)blockIdx.x * 32 >= rl) return;  // block-uniform
-  lloyd_reduce_body(fits.rec[g], G, rl, fits.out[g]);
+  rec_reduce_body(rec, G, rl, out);
 }
 
 // ============================================================== farthest
@@ -1202,125 +706,6 @@ int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu, const d
                          p.bsum_of(c, T), nullptr, as_stream(stream));
 }
 
-size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
-  return (size_t)kblocks(S) * lloyd_rec(k, F) * sizeof(double) + 256;
-}
-
-int mw_lloyd_step(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
-                  const float* d_centers, int k, uint8_t* d_labels, int mode, void* d_ws,
-                  void* stream) {
-  MW_CHECK_ARG(d_X && d_a && d_b && d_centers && d_labels && d_ws, "mw_lloyd_step: null pointer");
-  MW_CHECK_ARG(S > 0 && F > 0 && k >= 1, "mw_lloyd_step: bad shape");
-  MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_step: bad mode");
-  if (k > 64 || F > 64) {
-    set_error("mw_lloyd_step: k=%d F=%d unsupported (k <= 64, F <= 64)", k, F);
-    return MW_EUNSUPPORTED;
-  }
-  hipStream_t s = as_stream(stream);
-  const int G = kblocks(S);
-  const int64_t R = krows(S);
-  double* rec = reinterpret_cast<double*>(d_ws);
-  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
-  const int MBv = k <= 16 ? 1 : k <= 32 ? 2 : 4;
-  const size_t cent = cent_t_bytes(64, FM);
-  const size_t blk = ((size_t)k * F * 8 + 15) & ~(size_t)15;
-  const size_t lds = cent + blk + 4 * lloyd_wave_bytes(FM);
-#define MW_LLM(FMV, MBV, MO)                                                                   \
-  hipLaunchKernelGGL((lloyd_kernel<FMV, MBV, MO>), dim3(G), dim3(256), lds, s, d_X, S, F, d_a, \
-                     d_b, d_centers, k, d_labels, R, rec)
-#define MW_LL(FMV, MBV)              \
-  if (mode == 0) MW_LLM(FMV, MBV, 0); \
-  else if (mode == 1) MW_LLM(FMV, 1, 1); \
-  else MW_LLM(FMV, 1, 2);
-#define MW_LLF(FMV)                \
-  if (MBv == 1) { MW_LL(FMV, 1) }     \
-  else if (MBv == 2) { MW_LL(FMV, 2) } \
-  else { MW_LL(FMV, 4) }
-  if (FM == 8) { MW_LLF(8) }
-  else if (FM == 16) { MW_LLF(16) }
-  else if (FM == 32) { MW_LLF(32) }
-  else { MW_LLF(64) }
-#undef MW_LLF
-#undef MW_LL
-#undef MW_LLM
-  MW_LAUNCH_CHECK();
-  return MW_OK;
-}
-
-int mw_lloyd_reduce(const void* d_ws, int64_t S, int k, int F, double* d_out, void* stream) {
-  MW_CHECK_ARG(d_ws && d_out, "mw_lloyd_reduce: null pointer");
-  const int rl = lloyd_rec(k, F);
-  hipLaunchKernelGGL(lloyd_reduce_kernel, dim3((rl + 31) / 32), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<const double*>(d_ws), kblocks(S), rl, d_out);
-  MW_LAUNCH_CHECK();
-  return MW_OK;
-}
-
-int mw_lloyd_step_multi(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
-                        int n, const float* const* h_centers, const int* h_k,
-                        uint8_t* const* h_labels, int mode, void* const* h_ws, double* const* h_out,
-                        void* stream) {
-  MW_CHECK_ARG(d_X && d_a && d_b && h_centers && h_k && h_labels && h_ws && h_out,
-               "mw_lloyd_step_multi: null pointer");
-  MW_CHECK_ARG(S > 0 && F > 0 && n >= 1 && n <= kMaxFits, "mw_lloyd_step_multi: bad shape (n <= %d)",
-               kMaxFits);
-  MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_step_multi: bad mode");
-  LloydFits fits{};
-  int kmax = 0;
-  for (int g = 0; g < n; ++g) {
-    MW_CHECK_ARG(h_centers[g] && h_labels[g] && h_ws[g] && h_out[g] && h_k[g] >= 1,
-                 "mw_lloyd_step_multi: fit %d: bad arguments", g);
-    fits.centers[g] = h_centers[g];
-    fits.labels[g] = h_labels[g];
-    fits.rec[g] = reinterpret_cast<double*>(h_ws[g]);
-    fits.out[g] = h_out[g];
-    fits.k[g] = h_k[g];
-    kmax = h_k[g] > kmax ? h_k[g] : kmax;
-  }
-  if (kmax > 64 || F > 64) {
-    set_error("mw_lloyd_step_multi: k=%d F=%d unsupported (k <= 64, F <= 64)", kmax, F);
-    return MW_EUNSUPPORTED;
-  }
-  const int MBv = kmax <= 16 ? 1 : kmax <= 32 ? 2 : 4;
-  for (int g = 0; g < n; ++g)  // one M-step block shape per launch
-    if ((h_k[g] <= 16 ? 1 : h_k[g] <= 32 ? 2 : 4) != MBv) {
-      set_error("mw_lloyd_step_multi: fits mix k <= 16 / 17..32 / > 32 in one launch");
-      return MW_EINVAL;
-    }
-  hipStream_t s = as_stream(stream);
-  const int G = kblocks(S);
-  const int64_t R = krows(S);
-  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
-  const size_t cent = cent_t_bytes(64, FM);
-  const size_t blk = ((size_t)kmax * F * 8 + 15) & ~(size_t)15;
-  const size_t lds = cent + blk + 4 * lloyd_wave_bytes(FM);
-  const dim3 grid((unsigned)G * (unsigned)n);
-#define MW_LLM(FMV, MBV, MO)                                                                      \
-  hipLaunchKernelGGL((lloyd_multi_kernel<FMV, MBV, MO>), grid, dim3(256), lds, s, d_X, S, F, d_a, \
-                     d_b, fits, n, R)
-#define MW_LL(FMV, MBV)              \
-  if (mode == 0) MW_LLM(FMV, MBV, 0); \
-  else if (mode == 1) MW_LLM(FMV, 1, 1); \
-  else MW_LLM(FMV, 1, 2);
-#define MW_LLF(FMV)                \
-  if (MBv == 1) { MW_LL(FMV, 1) }     \
-  else if (MBv == 2) { MW_LL(FMV, 2) } \
-  else { MW_LL(FMV, 4) }
-  if (FM == 8) { MW_LLF(8) }
-  else if (FM == 16) { MW_LLF(16) }
-  else if (FM == 32) { MW_LLF(32) }
-  else { MW_LLF(64) }
-#undef MW_LLF
-#undef MW_LL
-#undef MW_LLM
-  MW_LAUNCH_CHECK();
-  const int rlmax = lloyd_rec(kmax, F);
-  hipLaunchKernelGGL(lloyd_reduce_multi_kernel, dim3((rlmax + 31) / 32, n), dim3(256), 0, s, fits, G,
-                     F);
-  MW_LAUNCH_CHECK();
-  return MW_OK;
-}
-
 size_t mw_farthest_ws_bytes(int64_t S) {
   return al256((size_t)S * sizeof(double)) + 1024 * (sizeof(double) + sizeof(int64_t)) + 256;
 }
@@ -1410,7 +795,7 @@ int mw_domain_records(const int8_t* d_label, const float* d_conf, int64_t n_pix,
 
 int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom, void* stream) {
   MW_CHECK_ARG(d_ws && d_dom && k >= 1, "mw_assign_reduce: bad args");
-  hipLaunchKernelGGL(lloyd_reduce_kernel, dim3((2 * k + 31) / 32), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(rec_reduce_kernel, dim3((2 * k + 31) / 32), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), kblocks(n_pix), 2 * k, d_dom);
   MW_LAUNCH_CHECK();
   return MW_OK;

@@ -1,0 +1,625 @@
+// The Lloyd iteration of sklearn's KMeans (lloyd_iter_chunked_dense,
+// _k_means_lloyd.pyx:23-218; _inertia_dense, _k_means_common.pyx:94-124) for
+// one or several fits over the same rows (the k sweep of find_optimal_k,
+// MILWRM.py:29-90), on MI355X (gfx950, wave64).
+//
+// E-step with distance bounds (Hamerly): per row the pass keeps ub >= the
+// distance to its own center and lb <= the distance to the second closest.
+// Between passes the centers move by drift_j, so ub += drift_label and lb -=
+// max_j drift_j; a row whose ub is below max(lb, half the separation of its
+// center from the nearest other center) by a relative margin kEps keeps its
+// label without reading its features.  The margin (1e-4) is far above the
+// fp32 rounding of the distances (F * 2^-24), so a skipped row always gets
+// the label the full computation would give it: labels are exactly those of
+// the plain argmin (strict '<', lowest index on ties).  Rows that fail the
+// test are read, their own-center distance tightens ub (second test), and
+// rows still undecided get all k distances.
+//
+// M-step, incremental and exact: every raw feature value is rounded once to a
+// per-feature fixed point, q = rint(x * 2^e_f) with |q| < 2^41 (e_f from the
+// column's max |x|), and a row whose label changes moves its q from the old
+// label's sums to the new one's as int64 adds.  Integer sums do not depend on
+// order, so the per-cluster sums equal the full recomputation, bit for bit,
+// whatever the partition of rows into blocks, tiles or ranks: results are
+// identical across 1 / 2 / 4 / 8 GPUs.  Per-block records carry each int64
+// as two integer-valued fp64 limbs (hi = floor(v / 2^32), lo = v - hi*2^32),
+// which the fixed-order fp64 fold and an RCCL fp64 all-reduce add exactly.
+// The host keeps the running sums (kmeans.py).
+//
+// Inertia (modes 1 and 2) in the same fixed point: per row rint(D * 2^e_d).
+#include <math.h>
+#include <stdlib.h>
+
+#include "kmeans_common.h"
+
+namespace mw {
+
+constexpr int kMaxFits = 24;
+constexpr float kEps = 1e-4f;  // bound-test margin (relative)
+
+struct LloydFitsArg {
+  mw_lloyd_fit f[kMaxFits];
+};
+
+__host__ __device__ inline int lloyd_rec(int k, int F) { return 2 * k * F + k + 4; }
+
+// x as an exact fixed-point integer: rint(x * 2^e) (|x * 2^e| < 2^41; fp64
+// holds it exactly, and sums of up to 2^12 of them)
+__device__ __forceinline__ double fixq64(float x, int e) { return rint(ldexp((double)x, e)); }
+__device__ __forceinline__ long long fixq(float x, int e) { return (long long)fixq64(x, e); }
+
+// int64 -> (hi, lo) integer-valued fp64 limbs
+__device__ __forceinline__ void limbs(long long v, double& hi, double& lo) {
+  const long long h = v >> 32;  // arithmetic shift: floor
+  hi = (double)h;
+  lo = (double)(v - h * (1LL << 32));
+}
+
+// squared distance of the scaled row to one center (the same fp32 chain as
+// nearest_centers: even features in .x, odd in .y, then .x + .y)
+template <int FMAX>
+__device__ __forceinline__ float dist_one(const f2v (&x2)[FMAX / 2], const f2v* cT, int j) {
+  f2v acc = f2v{0.f, 0.f};
+#pragma unroll
+  for (int p = 0; p < FMAX / 2; ++p) {
+    const f2v d = x2[p] - cT[p * 64 + j];
+    acc = __builtin_elementwise_fma(d, d, acc);
+  }
+  return acc.x + acc.y;
+}
+
+// bytes of one wave's row tile (64 rows x FMAX floats)
+__host__ __device__ inline size_t lloyd_tile_bytes(int FMAX) { return (size_t)64 * FMAX * 4; }
+
+constexpr int kChunk = 4096;  // rows per bound-test chunk (sparse passes): queue of u16 offsets
+
+// small per-block LDS state (size a multiple of 16 bytes)
+struct alignas(16) LloydSmall {
+  float a[64], b[64];
+  int e[64];
+  float drift[64], half[64];
+  int cnt[64];
+  double red[4];
+  long long red64[4];
+  int qn, pad[3];
+};
+
+// LDS of one block: LloydSmall | pair-major centers | cluster sums k x F (int64, mode 0) |
+// per-wave row tiles | per-wave labels (64 int) | chunk queue (sparse mode 0)
+__host__ __device__ inline size_t lloyd_lds_bytes(int FMAX, int k, int F, int mode, int kind) {
+  size_t b = sizeof(LloydSmall) + cent_t_bytes(64, FMAX);
+  if (mode == 0) b += ((size_t)k * F * 8 + 15) & ~(size_t)15;
+  b += 4 * (lloyd_tile_bytes(FMAX) + 64 * 4);
+  if (mode == 0 && kind == 2) b += (size_t)kChunk * 2;  // kQueue
+  return b;
+}
+
+// Kinds of mode-0 pass (mw_lloyd_pass `kind`):
+constexpr int kFirst = 0;  // every row unlabelled: full E-step, sums of all rows
+constexpr int kTile = 1;   // stream every tile's rows; bounds skip the E-step per lane
+constexpr int kQueue = 2;  // stream only the row state; read the undecided rows
+constexpr int kFirstAtomic = 3;  // kFirst with the sums by LDS atomics (A/B)
+
+// One pass of fit g = blockIdx.x % n over row block blockIdx.x / n (the n
+// blocks that read one row block are dispatched together: rows that several
+// fits read come from the on-die caches).
+//   MODE 0, kFirst: full E-step over streamed 64-row tiles; the cluster sums
+//     of each tile's rows as a one-hot GEMM on the fp64 matrix cores
+//     (A[label][row] = 1, B[row][f] = q(x_f): integer products and sums below
+//     2^53 are exact), flushed to int64 every 32 tiles.
+//   MODE 0, kTile: streamed tiles with the row state; the bound test per row,
+//     the own-center distance for undecided rows, all k distances where still
+//     undecided; changed rows move their q between cluster sums (LDS int64
+//     atomics, lane = feature).  For passes where most rows are undecided.
+//   MODE 0, kQueue: per chunk of kChunk rows the bound test streams only the
+//     row state (4 rows per lane) and queues the rows it cannot decide; waves
+//     gather the queued rows 64 at a time and finish them as kTile does.  For
+//     passes where few rows are undecided.
+//   MODE 1: full E-step (labels updated) + inertia of the new labels
+//   MODE 2: inertia of the current labels
+template <int FMAX, int MODE, int KIND>
+__global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict__ X, int64_t S, int F,
+                                                         const float* __restrict__ ga,
+                                                         const float* __restrict__ gb,
+                                                         const int* __restrict__ qexp,
+                                                         const LloydFitsArg fits, int n, int64_t R) {
+  constexpr int NV = FMAX / 4;
+  constexpr int RP = 64 / FMAX;  // changed rows folded per M-step round (lane = row slot x feature)
+  constexpr int NB = FMAX <= 16 ? 1 : FMAX / 16;  // 16-feature MFMA column blocks
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int g = blockIdx.x % n, blk = blockIdx.x / n;
+  const mw_lloyd_fit& fit = fits.f[g];
+  const int k = fit.k;
+  const int iexp = fit.inertia_exp;
+  const int t = threadIdx.x, lane = t & 63, nw = blockDim.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  // every LDS variable lives in the dynamic region at 16-byte aligned offsets
+  // (static __shared__ would shift the dynamic base off 16 bytes:
+  // misaligned 8-byte accesses replay, misaligned 64-bit atomics are unsafe)
+  char* sp = smem;
+  LloydSmall* sm = reinterpret_cast<LloydSmall*>(sp);
+  sp += sizeof(LloydSmall);
+  float* s_a = sm->a;
+  float* s_b = sm->b;
+  int* s_e = sm->e;
+  float* s_drift = sm->drift;
+  float* s_half = sm->half;
+  int* s_cnt = sm->cnt;
+  int& s_qn = sm->qn;
+  double* s_red = sm->red;
+  long long* s_red64 = sm->red64;
+  f2v* s_cT = reinterpret_cast<f2v*>(sp);
+  sp += cent_t_bytes(64, FMAX);
+  unsigned long long* s_acc = reinterpret_cast<unsigned long long*>(sp);
+  if (MODE == 0) sp += ((size_t)k * F * 8 + 15) & ~(size_t)15;
+  float* s_tile = reinterpret_cast<float*>(sp + (size_t)wid * lloyd_tile_bytes(FMAX));
+  sp += 4 * lloyd_tile_bytes(FMAX);
+  int* s_lab = reinterpret_cast<int*>(sp) + wid * 64;
+  sp += 4 * 64 * 4;
+  uint16_t* s_q = reinterpret_cast<uint16_t*>(sp);
+
+  load_centers_T<FMAX, 64>(fit.centers, k, F, s_cT);
+  for (int f = t; f < 64; f += blockDim.x) {
+    s_a[f] = f < F ? ga[f] : 0.f;  // padded features scale to exactly 0
+    s_b[f] = f < F ? gb[f] : 0.f;
+    s_e[f] = f < F ? qexp[f] : 0;
+  }
+  constexpr bool BOUNDS = MODE == 0 && (KIND == kTile || KIND == kQueue);
+  for (int j = t; j < 64; j += blockDim.x) {
+    s_drift[j] = (BOUNDS && j < k) ? fit.drift[j] : 0.f;
+    s_half[j] = (BOUNDS && j < k) ? fit.half_sep[j] : 0.f;
+    s_cnt[j] = 0;
+  }
+  if (t == 0) s_qn = 0;
+  if (MODE == 0)
+    for (int q = t; q < k * F; q += blockDim.x) s_acc[q] = 0ull;
+  __syncthreads();
+  const float dmax = fit.drift_max;
+
+  const int64_t lo = (int64_t)blk * R, hi = min(S, lo + R);
+  const int64_t total = S * (int64_t)F, n4 = total >> 2;
+  const int64_t nb = hi > lo ? hi - lo : 0;
+  uint8_t* __restrict__ labels = fit.labels;
+  float* __restrict__ ubuf = fit.ub;
+  float* __restrict__ lbuf = fit.lb;
+  long long changed = 0, recomputed = 0, inert = 0;
+
+  // ---- M-step of the changed rows of the wave's tile (lane = row slot x feature) ----
+  auto move_rows = [&](unsigned long long cm, int lab, int lab_old) {
+    const int sub = lane / FMAX, f = lane - sub * FMAX;
+    while (cm != 0ull) {  // wave-uniform
+      int jsel = -1;
+#pragma unroll
+      for (int r = 0; r < RP; ++r) {
+        if (cm != 0ull) {
+          const int j = __builtin_ctzll(cm);
+          cm &= cm - 1ull;
+          if (sub == r) jsel = j;
+        }
+      }
+      const int jj = jsel < 0 ? 0 : jsel;
+      const int ln = __shfl(lab, jj, 64), lo_ = __shfl(lab_old, jj, 64);
+      if (jsel >= 0 && f < F) {
+        const long long q = fixq(s_tile[jj * F + f], s_e[f]);
+        atomicAdd(&s_acc[ln * F + f], (unsigned long long)q);
+        if (lo_ < k) atomicAdd(&s_acc[lo_ * F + f], (unsigned long long)(-q));
+        if (f == 0) {
+          atomicAdd(&s_cnt[ln], 1);
+          if (lo_ < k) atomicAdd(&s_cnt[lo_], -1);
+        }
+      }
+    }
+  };
+  // ---- the undecided rows of a staged tile: tighten, full E-step, state, sums ----
+  // (lane = row of the tile; `need`: the drifted bounds did not decide the row)
+  auto finish_rows = [&](bool valid, bool need, int lab_old, float ub, float lbv, float thr,
+                         auto&& store) {
+    const bool has_old = lab_old < k;
+    const int la = has_old ? lab_old : 0;
+    f2v x2[FMAX / 2];
+    load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
+    const float da = dist_one<FMAX>(x2, s_cT, la);
+    bool need2 = need;
+    if (need && has_old) {
+      ub = sqrtf(da);
+      need2 = !(ub * (1.f + kEps) < thr);
+    }
+    int lab = lab_old;
+    if (__ballot(need2) != 0ull) {
+      int ln;
+      float m1, m2;
+      nearest_centers<FMAX, 64, true>(x2, s_cT, k, ln, m1, m2);
+      if (need2) {
+        lab = ln;
+        ub = sqrtf(m1);
+        lbv = k > 1 ? sqrtf(m2) : __builtin_inff();
+        recomputed += 1;
+      }
+    }
+    const bool ch = valid && lab != lab_old;
+    changed += ch ? 1 : 0;
+    store(valid, ch, lab, ub, lbv);
+    move_rows(__ballot(ch), lab, lab_old);
+  };
+
+  if constexpr (MODE == 0 && KIND == kQueue) {
+    // =========================== queue pass ===========================
+    for (int64_t c0 = lo; c0 < hi; c0 += kChunk) {
+      const int clen = (int)min((int64_t)kChunk, hi - c0);
+      // ---- phase 1: bound test, 4 consecutive rows per lane, queue the undecided ----
+      for (int base = wid * 256; base < clen; base += nw * 256) {
+        const int off0 = base + 4 * lane;
+        const int64_t r0 = c0 + off0;
+        uint32_t lab4;
+        f4v ub4, lb4;
+        if (off0 + 3 < clen && (r0 & 3) == 0) {
+          lab4 = *reinterpret_cast<const uint32_t*>(labels + r0);
+          ub4 = *reinterpret_cast<const f4v*>(ubuf + r0);
+          lb4 = *reinterpret_cast<const f4v*>(lbuf + r0);
+        } else {
+          lab4 = 0xFFFFFFFFu;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (off0 + i < clen) {
+              lab4 = (lab4 & ~(0xFFu << (8 * i))) | ((uint32_t)labels[r0 + i] << (8 * i));
+              ub4[i] = ubuf[r0 + i];
+              lb4[i] = lbuf[r0 + i];
+            }
+          }
+        }
+        bool skip[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lab_old = (lab4 >> (8 * i)) & 0xFF;
+          const int la = lab_old < k ? lab_old : 0;
+          const float ub = ub4[i] + s_drift[la];
+          const float lbv = lb4[i] - dmax;
+          const float thr = fmaxf(lbv, s_half[la]);
+          const bool valid = off0 + i < clen;
+          const bool need = valid && (lab_old >= k || !(ub * (1.f + kEps) < thr));
+          skip[i] = valid && !need;
+          ub4[i] = ub;
+          lb4[i] = lbv;
+          const unsigned long long m = __ballot(need);
+          if (m != 0ull) {
+            int qb = 0;
+            if (lane == 0) qb = atomicAdd(&s_qn, __popcll(m));
+            qb = __shfl(qb, 0, 64);
+            if (need) s_q[qb + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(off0 + i);
+          }
+        }
+        if (skip[0] && skip[1] && skip[2] && skip[3] && off0 + 3 < clen && (r0 & 3) == 0) {
+          *reinterpret_cast<f4v*>(ubuf + r0) = ub4;
+          *reinterpret_cast<f4v*>(lbuf + r0) = lb4;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (skip[i]) {
+              ubuf[r0 + i] = ub4[i];
+              lbuf[r0 + i] = lb4[i];
+            }
+        }
+      }
+      __syncthreads();
+      const int nq = s_qn;
+      // ---- phase 2: the queued rows, 64 per wave batch ----
+      for (int e0 = wid * 64; e0 < nq; e0 += nw * 64) {
+        const int cnt_b = min(64, nq - e0);
+        const bool valid = lane < cnt_b;
+        const int64_t r = c0 + s_q[e0 + (valid ? lane : 0)];
+        // gather the batch's rows into the wave tile (row j at s_tile + j*F)
+        if ((F & 1) == 0) {
+          const int P2 = F >> 1;
+          int j = lane / P2, c = lane - (lane / P2) * P2;  // piece (j, c) = p, stepped by 64
+          const int dj = 64 / P2, dc = 64 - dj * P2;
+          for (int p = lane; p < 64 * P2; p += 64) {
+            const int64_t rj = c0 + s_q[e0 + (j < cnt_b ? j : 0)];
+            *reinterpret_cast<f2v*>(s_tile + j * F + 2 * c) = *reinterpret_cast<const f2v*>(X + rj * F + 2 * c);
+            j += dj;
+            c += dc;
+            if (c >= P2) { c -= P2; ++j; }
+          }
+        } else {
+          for (int p = lane; p < 64 * F; p += 64) {
+            const int j = p / F, c = p - j * F;
+            const int64_t rj = c0 + s_q[e0 + (j < cnt_b ? j : 0)];
+            s_tile[j * F + c] = X[rj * F + c];
+          }
+        }
+        const int lab_old = labels[r];
+        const int la = lab_old < k ? lab_old : 0;
+        const float ub = ubuf[r] + s_drift[la];
+        const float lbv = lbuf[r] - dmax;
+        const float thr = fmaxf(lbv, s_half[la]);
+        finish_rows(valid, valid, lab_old, ub, lbv, thr,
+                    [&](bool v, bool ch, int lab, float u, float l) {
+                      if (v) {
+                        if (ch) labels[r] = (uint8_t)lab;
+                        ubuf[r] = u;
+                        lbuf[r] = l;
+                      }
+                    });
+      }
+      __syncthreads();
+      if (t == 0) s_qn = 0;
+      __syncthreads();
+    }
+  } else {
+    // ========================== streamed tiles ==========================
+    const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + lo * F, (S - lo) * F * 4);
+    const __amdgpu_buffer_rsrc_t rl = make_rsrc(labels + lo, nb);
+    const __amdgpu_buffer_rsrc_t ru = make_rsrc(ubuf ? (void*)(ubuf + lo) : (void*)X, ubuf ? nb * 4 : 0);
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(lbuf ? (void*)(lbuf + lo) : (void*)X, lbuf ? nb * 4 : 0);
+    const int tile_bytes = 64 * F * 4;
+    const int kk = lane >> 4, mm = lane & 15;  // MFMA operand lane map
+    constexpr int MBX = 4;                     // label blocks of 16 kept in fp64 accumulators
+    const int MB = (k + 15) >> 4;
+    const bool mfma_m = MODE == 0 && KIND == kFirst && MB * NB <= MBX;
+    static_assert(KIND != kFirstAtomic || MODE == 0, "atomic first pass is mode 0");
+    typedef double d4v __attribute__((ext_vector_type(4)));
+    d4v acc[KIND == kFirst && MODE == 0 ? MBX : 1];
+#pragma unroll
+    for (int i = 0; i < (KIND == kFirst && MODE == 0 ? MBX : 1); ++i) acc[i] = d4v{0.0, 0.0, 0.0, 0.0};
+    int since_flush = 0;
+    auto flush = [&]() {
+      if constexpr (MODE == 0 && KIND == kFirst) {
+        if (!mfma_m) return;
+#pragma unroll
+        for (int i = 0; i < MBX; ++i) {
+          if (i < MB * NB) {
+            const int mb = i / NB, nbk = i - mb * NB;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int lab_i = 16 * mb + kk + 4 * r, f = 16 * nbk + mm;  // f64 D map: row (l>>4)+4r, col l&15
+              if (lab_i < k && f < F && acc[i][r] != 0.0)
+                atomicAdd(&s_acc[lab_i * F + f], (unsigned long long)(long long)acc[i][r]);
+            }
+          }
+          acc[i] = d4v{0.0, 0.0, 0.0, 0.0};
+        }
+      }
+    };
+
+    f4v v[NV];
+    int lab_next = 0;
+    float ub_next = 0.f, lb_next = 0.f;
+    auto fetch = [&](int tt) {
+      tt = tt < ntile ? tt : ntile - 1;
+      lab_next = __builtin_amdgcn_raw_buffer_load_b8(rl, lane, tt * 64, 0);
+      if (BOUNDS) {
+        ub_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ru, lane * 4, tt * 256, 0));
+        lb_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, lane * 4, tt * 256, 0));
+      }
+      tile_load<NV>(rx, tt * tile_bytes, lane, v);
+    };
+    int tc = wid;
+    if (tc < ntile) fetch(tc);
+    for (; tc < ntile; tc += nw) {
+      const int64_t r0 = lo + (int64_t)tc * 64;
+      const int nrow = (int)min((int64_t)64, hi - r0);
+      const bool valid = lane < nrow;
+      const int lab_old = lab_next;
+      const float ub_in = ub_next, lb_in = lb_next;
+      {
+        f4v* s4 = reinterpret_cast<f4v*>(s_tile);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) s4[lane + i * 64] = v[i];
+      }
+      wt_tail(nrow * F, r0 * F, n4, X, total, s_tile, lane);
+      fetch(tc + nw);  // the next tile's loads stay in flight during this tile
+      if constexpr (BOUNDS) {
+        // ---- kTile: bound test, then finish the undecided rows ----
+        const int la = lab_old < k ? lab_old : 0;
+        const float ub = ub_in + s_drift[la];
+        const float lbv = lb_in - dmax;
+        const float thr = fmaxf(lbv, s_half[la]);
+        const bool need = valid && (lab_old >= k || !(ub * (1.f + kEps) < thr));
+        auto store = [&](bool v, bool ch, int lab, float u, float l) {
+          if (v) {
+            if (ch) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)lab, rl, lane, tc * 64, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, u), ru, lane * 4, tc * 256, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, l), rw, lane * 4, tc * 256, 0);
+          }
+        };
+        if (__ballot(need) != 0ull) finish_rows(valid, need, lab_old, ub, lbv, thr, store);
+        else store(valid, false, lab_old, ub, lbv);
+        continue;
+      } else {
+        f2v x2[FMAX / 2];
+        load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
+        if (MODE == 2) {
+          const float d = dist_one<FMAX>(x2, s_cT, lab_old < k ? lab_old : 0);
+          if (valid) inert += fixq(d, iexp);
+          continue;
+        }
+        int lab;
+        float m1, m2;
+        nearest_centers<FMAX, 64, true>(x2, s_cT, k, lab, m1, m2);
+        recomputed += valid ? 1 : 0;
+        const bool ch = valid && lab != lab_old;
+        changed += ch ? 1 : 0;
+        if (valid) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)lab, rl, lane, tc * 64, 0);
+        if (MODE == 1) {
+          if (valid) inert += fixq(m1, iexp);
+          continue;
+        }
+        // ---- MODE 0 kFirst: bounds, sizes, sums ----
+        if (valid) {
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, sqrtf(m1)), ru, lane * 4, tc * 256, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(
+              __builtin_bit_cast(int, k > 1 ? sqrtf(m2) : __builtin_inff()), rw, lane * 4, tc * 256, 0);
+        }
+        if constexpr (MODE == 0 && KIND == kFirstAtomic) {
+          move_rows(__ballot(ch), lab, 255);
+          continue;
+        }
+        if constexpr (MODE == 0 && KIND == kFirst) {
+          if (!mfma_m) {
+            move_rows(__ballot(ch), lab, 255);
+            continue;
+          }
+          if (valid) atomicAdd(&s_cnt[lab], 1);
+          s_lab[lane] = valid ? lab : -1;
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int st = 0; st < 16; ++st) {  // k-steps of 4 rows
+            const int row = 4 * st + kk;
+            const int lr = s_lab[row];
+            double bq[NB];
+#pragma unroll
+            for (int nbk = 0; nbk < NB; ++nbk) {
+              const int f = 16 * nbk + mm;
+              bq[nbk] = f < F ? fixq64(s_tile[row * F + f], s_e[f]) : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < MBX; ++i) {
+              if (i < MB * NB) {
+                const int mb = i / NB, nbk = i - mb * NB;
+                const double a = lr == 16 * mb + mm ? 1.0 : 0.0;
+                acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq[nbk], acc[i], 0, 0, 0);
+              }
+            }
+          }
+          if (++since_flush == 32) {  // sums stay below 32 * 64 * 2^41 = 2^52: exact
+            flush();
+            since_flush = 0;
+          }
+        }
+      }
+    }
+    flush();
+  }
+  // ---- block record: [dQ_hi kF | dQ_lo kF | dcount k | changed | recomputed | in_hi | in_lo] ----
+  const double ch = block_sum((double)changed, s_red);
+  const double rc = block_sum((double)recomputed, s_red);
+  const long long in = block_sum(inert, s_red64);
+  __syncthreads();
+  const int rlen = lloyd_rec(k, F);
+  double* out = reinterpret_cast<double*>(fit.ws) + (size_t)blk * rlen;
+  if (MODE == 0) {
+    for (int q = t; q < k * F; q += blockDim.x) {
+      double h, l;
+      limbs((long long)s_acc[q], h, l);
+      out[q] = h;
+      out[k * F + q] = l;
+    }
+    for (int j = t; j < k; j += blockDim.x) out[2 * k * F + j] = (double)s_cnt[j];
+  } else {
+    for (int q = t; q < 2 * k * F + k; q += blockDim.x) out[q] = 0.0;
+  }
+  if (t == 0) {
+    double h, l;
+    limbs(in, h, l);
+    out[2 * k * F + k] = ch;
+    out[2 * k * F + k + 1] = rc;
+    out[2 * k * F + k + 2] = h;
+    out[2 * k * F + k + 3] = l;
+  }
+}
+
+// one fit per blockIdx.y: fixed-order fold of its G block records
+__global__ void __launch_bounds__(256) lloyd_reduce_fits_kernel(const LloydFitsArg fits, int G, int F) {
+  const mw_lloyd_fit& fit = fits.f[blockIdx.y];
+  const int rl = lloyd_rec(fit.k, F);
+  if ((int)blockIdx.x * 32 >= rl) return;  // block-uniform
+  rec_reduce_body(reinterpret_cast<const double*>(fit.ws), G, rl, fit.out);
+}
+
+// ---- column max |x| (fixed-point exponents of the M-step) ----
+__global__ void __launch_bounds__(256) col_absmax_kernel(const float* __restrict__ X, int64_t S, int F,
+                                                         unsigned* __restrict__ out) {
+  __shared__ unsigned s_m[256];
+  for (int f = threadIdx.x; f < 256; f += blockDim.x) s_m[f] = 0u;
+  __syncthreads();
+  const int64_t total = S * (int64_t)F;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // element e = row * F + f: each thread walks a fixed residue class of F
+  // only when stride % F == 0; otherwise it recomputes f per element
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const float x = fabsf(X[e]);
+    const int f = (int)(e % F);
+    atomicMax(&s_m[f], __builtin_bit_cast(unsigned, x));  // non-negative floats order as their bits
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < F; f += blockDim.x) atomicMax(&out[f], s_m[f]);
+}
+
+}  // namespace mw
+
+using namespace mw;
+
+extern "C" {
+
+int mw_lloyd_rec_len(int k, int F) { return lloyd_rec(k, F); }
+
+size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
+  return (size_t)kblocks(S) * lloyd_rec(k, F) * sizeof(double) + 256;
+}
+
+int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream) {
+  MW_CHECK_ARG(d_X && d_out && S > 0 && F > 0 && F <= 256, "mw_col_absmax: bad arguments");
+  hipStream_t s = as_stream(stream);
+  MW_HIP(hipMemsetAsync(d_out, 0, sizeof(float) * F, s));
+  const int64_t total = S * (int64_t)F;
+  const int nb = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL(col_absmax_kernel, dim3(nb), dim3(256), 0, s, d_X, S, F,
+                     reinterpret_cast<unsigned*>(d_out));
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
+                  const int32_t* d_qexp, int n, const mw_lloyd_fit* h_fits, int mode, int kind,
+                  void* stream) {
+  MW_CHECK_ARG(d_X && d_a && d_b && d_qexp && h_fits, "mw_lloyd_pass: null pointer");
+  MW_CHECK_ARG(S > 0 && F > 0 && n >= 1 && n <= kMaxFits, "mw_lloyd_pass: bad shape (1 <= n <= %d)",
+               kMaxFits);
+  MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_pass: bad mode %d", mode);
+  MW_CHECK_ARG(kind >= 0 && kind <= 3, "mw_lloyd_pass: bad kind %d", kind);
+  if (mode != 0) kind = kFirst;  // modes 1 and 2 stream every tile
+  LloydFitsArg fits{};
+  int kmax = 0;
+  for (int g = 0; g < n; ++g) {
+    const mw_lloyd_fit& f = h_fits[g];
+    MW_CHECK_ARG(f.centers && f.labels && f.ws && f.out && f.k >= 1, "mw_lloyd_pass: fit %d: bad arguments", g);
+    MW_CHECK_ARG(mode != 0 || (f.ub && f.lb && f.drift && f.half_sep),
+                 "mw_lloyd_pass: fit %d: mode 0 needs ub, lb, drift, half_sep", g);
+    fits.f[g] = f;
+    kmax = f.k > kmax ? f.k : kmax;
+  }
+  if (kmax > 64 || F > 64) {
+    set_error("mw_lloyd_pass: k=%d F=%d unsupported (k <= 64, F <= 64)", kmax, F);
+    return MW_EUNSUPPORTED;
+  }
+  hipStream_t s = as_stream(stream);
+  const int G = kblocks(S);
+  const int64_t R = krows(S);
+  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
+  const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
+  const dim3 grid((unsigned)G * (unsigned)n);
+#define MW_LP(FMV, MO, KI)                                                                          \
+  hipLaunchKernelGGL((lloyd_pass_kernel<FMV, MO, KI>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, \
+                     d_qexp, fits, n, R)
+#define MW_LPF(FMV)                                 \
+  if (mode == 0) {                                  \
+    if (kind == kFirst) MW_LP(FMV, 0, kFirst);      \
+    else if (kind == kTile) MW_LP(FMV, 0, kTile);   \
+    else if (kind == kFirstAtomic) MW_LP(FMV, 0, kFirstAtomic); \
+    else MW_LP(FMV, 0, kQueue);                     \
+  } else if (mode == 1) MW_LP(FMV, 1, kFirst);      \
+  else MW_LP(FMV, 2, kFirst);
+  if (FM == 8) { MW_LPF(8) }
+  else if (FM == 16) { MW_LPF(16) }
+  else if (FM == 32) { MW_LPF(32) }
+  else { MW_LPF(64) }
+#undef MW_LPF
+#undef MW_LP
+  MW_LAUNCH_CHECK();
+  const int rlmax = lloyd_rec(kmax, F);
+  hipLaunchKernelGGL(lloyd_reduce_fits_kernel, dim3((rlmax + 31) / 32, n), dim3(256), 0, s, fits, G, F);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+}  // extern "C"

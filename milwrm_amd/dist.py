@@ -41,6 +41,9 @@ class LocalComm:
     def all_reduce_(self, t: torch.Tensor):
         return t
 
+    def all_reduce_max_np(self, a: np.ndarray) -> np.ndarray:
+        return np.asarray(a)
+
     def sharded(self) -> bool:
         return False
 
@@ -87,6 +90,11 @@ class DistComm(LocalComm):
         else:
             dist.all_reduce(t, group=self.group)
         return t
+
+    def all_reduce_max_np(self, a: np.ndarray) -> np.ndarray:
+        t = torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=self.device).clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t.cpu().numpy()
 
     # -- preprocessing statistics --------------------------------------
     def batch_stats(self, est, pix):

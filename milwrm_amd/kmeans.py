@@ -15,6 +15,8 @@ n_samples_seen_) computed from device column statistics (Chan merge, fp64).
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
 import warnings
 
 import numpy as np
@@ -38,9 +40,32 @@ class DeviceRows:
         dev = X.device
         self.mu64 = D.h2d(self.mu, dev)
         self.inv64 = D.h2d(self.inv, dev)
-        self.a32 = D.h2d(self.inv.astype(np.float32), dev)
-        self.b32 = D.h2d((-self.mu * self.inv).astype(np.float32), dev)
+        self.a_host = self.inv.astype(np.float32)
+        self.b_host = (-self.mu * self.inv).astype(np.float32)
+        self.a32 = D.h2d(self.a_host, dev)
+        self.b32 = D.h2d(self.b_host, dev)
         self._feature_var = feature_var
+        self.xmax = None      # per-feature max |x| over all rows (all shards)
+        self.qexp_dev = None  # fixed-point exponents of the Lloyd M-step (int32, device)
+
+    def fixed_point(self, comm=None) -> np.ndarray:
+        """Exponents e_f with max|x_f| * 2^e_f <= 2^40 (global over the shards
+        of ``comm``), uploaded once; returns the fp64 factors 2^-e_f that turn
+        a fixed-point sum back into a sum of x (lloyd.hip M-step)."""
+        if self.qexp_dev is None:
+            m = torch.empty(self.F, dtype=torch.float32, device=self.X.device)
+            if self.S:
+                N.call("mw_col_absmax", D.P(self.X), self.S, self.F, D.P(m), D.stream())
+                xmax = D.d2h(m).astype(np.float64)
+            else:
+                xmax = np.zeros(self.F)
+            if comm is not None and comm.sharded():
+                xmax = comm.all_reduce_max_np(xmax)
+            self.xmax = xmax.astype(np.float32)
+            e = np.array([_exp_below(float(v)) for v in xmax], dtype=np.int32)
+            self.qexp = e
+            self.qexp_dev = D.h2d(e, self.X.device)
+        return np.ldexp(1.0, -self.qexp.astype(np.int64)).astype(np.float64)
 
     @classmethod
     def from_host(cls, X: np.ndarray) -> "DeviceRows":
@@ -186,163 +211,328 @@ def _average_centers(centers, weight):
             centers[j] = centers[amax]
 
 
+def _round_f32(x, up: bool) -> np.ndarray:
+    """fp64 -> fp32 rounded toward +inf (up) or -inf (down), elementwise."""
+    x = np.asarray(x, dtype=np.float64)
+    f = x.astype(np.float32)
+    if up:
+        bad = f.astype(np.float64) < x
+        f[bad] = np.nextafter(f[bad], np.float32(np.inf))
+    else:
+        bad = f.astype(np.float64) > x
+        f[bad] = np.nextafter(f[bad], np.float32(-np.inf))
+    return f
+
+
+def _bound_tables(c32: np.ndarray, prev32):
+    """Per-center drift |c - c_prev| (rounded up), its max, and half the
+    separation to the nearest other center (rounded down), from the fp32
+    centers the device uses (lloyd.hip bound test).  MW_LLOYD_NOBOUND=1 (A/B
+    and parity checks) makes every bound test fail: full E-step each pass."""
+    c = c32.astype(np.float64)
+    if os.environ.get("MW_LLOYD_NOBOUND") == "1":
+        k = c.shape[0]
+        return np.full(k, np.inf, np.float32), float("inf"), np.zeros(k, np.float32)
+    k = c.shape[0]
+    drift = np.zeros(k) if prev32 is None else np.sqrt(((c - prev32.astype(np.float64)) ** 2).sum(1))
+    if k > 1:
+        d2 = ((c[:, None, :] - c[None, :, :]) ** 2).sum(-1)
+        np.fill_diagonal(d2, np.inf)
+        half = 0.5 * np.sqrt(d2.min(1))
+    else:
+        half = np.full(1, np.inf)
+    drift32 = _round_f32(drift, up=True)
+    return drift32, float(drift32.max()), _round_f32(half, up=False)
+
+
+def _exp_below(bound: float, bits: int = 40) -> int:
+    """e with bound * 2^e <= 2^bits (0 for bound 0)."""
+    if not np.isfinite(bound) or bound <= 0:
+        return 0
+    return bits - int(np.frexp(bound)[1])
+
+
+class _FitState:
+    """Host side of one Lloyd fit: fp64 centers, exact fixed-point cluster
+    sums (int64 hi/lo limbs, value = hi * 2^32 + lo) and sizes, device labels
+    and distance bounds."""
+
+    def __init__(self, rows, centers, dev):
+        S, F = rows.S, rows.F
+        self.k = k = int(centers.shape[0])
+        self.centers = np.array(centers, dtype=np.float64)
+        self.prev32 = None
+        self.q_hi = np.zeros((k, F), dtype=np.int64)
+        self.q_lo = np.zeros((k, F), dtype=np.int64)
+        self.count = np.zeros(k, dtype=np.int64)
+        self.labels = torch.full((S,), 255, dtype=torch.uint8, device=dev)  # 255 = no label yet
+        self.ub = torch.empty(S, dtype=torch.float32, device=dev)
+        self.lb = torch.empty(S, dtype=torch.float32, device=dev)
+        self.ws = torch.empty(N.query("mw_lloyd_ws_bytes", S, k, F), dtype=torch.uint8, device=dev)
+        self.done = False
+        self.strict = False
+        self.n_iter = 0
+        self.recomputed = 0
+        self.history = []  # (changed, recomputed) per pass
+        self.iexp = 0
+
+    def add(self, rec, F, qscale, a64, b64):
+        """Apply a pass's record (mode 0): exact sums, sizes; returns the
+        scaled per-cluster sums (fp64), the sizes and the changed count."""
+        k = self.k
+        hi = rec[:k * F].reshape(k, F).astype(np.int64)
+        lo = rec[k * F:2 * k * F].reshape(k, F).astype(np.int64)
+        self.q_hi += hi
+        self.q_lo += lo
+        carry = self.q_lo >> 32  # keep lo in [0, 2^32): every limb stays exact in fp64
+        self.q_hi += carry
+        self.q_lo -= carry << 32
+        self.count += rec[2 * k * F:2 * k * F + k].astype(np.int64)
+        tail = rec[2 * k * F + k:]
+        self.recomputed += int(tail[1])
+        self.history.append((int(tail[0]), int(tail[1])))
+        sums_x = (self.q_hi.astype(np.float64) * 4294967296.0 + self.q_lo.astype(np.float64)) * qscale
+        cnt = self.count.astype(np.float64)
+        return a64[None, :] * sums_x + b64[None, :] * cnt[:, None], cnt, tail[0]
+
+
+KIND_FIRST, KIND_TILE, KIND_QUEUE = 0, 1, 2
+# a mode-0 pass streams every row (kTile) while the previous pass recomputed
+# more than this fraction of the rows, else only the undecided ones (kQueue)
+QUEUE_BELOW = float(os.environ.get("MW_LLOYD_QUEUE_BELOW", "0.25"))
+
+
+def _launch_pass(rows, fits_g, mode, kind, par, poff, outs, st, label="lloyd_pass"):
+    """One mw_lloyd_pass over the rows for the fits in ``fits_g`` (list of
+    (g, _FitState)), records folded into ``outs[g]``."""
+    S, F = rows.S, rows.F
+    arr = (N.LloydFit * len(fits_g))()
+    nbytes = 0
+    for i, (g, fs) in enumerate(fits_g):
+        base = D.P(par) + int(poff[g]) * 4
+        k = fs.k
+        arr[i] = N.LloydFit(base, base + k * F * 4, base + (k * F + k) * 4, D.P(fs.labels),
+                            D.P(fs.ub), D.P(fs.lb), D.P(fs.ws), D.P(outs[g]), k,
+                            float(fs.drift_max), int(fs.iexp))
+        nbytes += S * 9 + (S * F * 4 if (mode or kind != KIND_QUEUE) else 0)
+    tag = "" if mode else ("_first", "_tile", "_queue", "_first_atomic")[kind]
+    ev = None
+    if TRACE is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    with profiling.timed(f"{label}_mode{mode}{tag}", nbytes):
+        N.call("mw_lloyd_pass", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(rows.qexp_dev),
+               len(fits_g), C.addressof(arr), int(mode), int(kind), st)
+    if ev is not None:
+        ev[1].record()
+        TRACE.append({"mode": mode, "kind": tag.strip("_"), "fits": [g for g, _ in fits_g], "ev": ev})
+
+
+TRACE = [] if os.environ.get("MW_LLOYD_TRACE") == "1" else None  # per-launch timing (diagnostics)
+
+
+def trace_summary(fits_hist=None):
+    """Resolve TRACE into [{mode, kind, n_fits, ms}] and clear it."""
+    if TRACE is None:
+        return []
+    torch.cuda.synchronize()
+    out = [{"mode": t["mode"], "kind": t["kind"], "n_fits": len(t["fits"]),
+            "ms": round(t["ev"][0].elapsed_time(t["ev"][1]), 4)} for t in TRACE]
+    TRACE.clear()
+    return out
+
+
+def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, comm=LOCAL):
+    """``_kmeans_single_lloyd`` (_kmeans.py:624-752) for one or several
+    independent fits over the same rows, run in lockstep: every iteration is
+    ONE mw_lloyd_pass for all the fits still running (up to 24 per launch),
+    one all-reduce and one device-to-host copy of their records.  Each fit's
+    arithmetic does not depend on which others run beside it, so a fit
+    returns exactly what it returns alone.  Returns a list of (labels u8
+    tensor, inertia, centers fp64, n_iter)."""
+    S, F = rows.S, rows.F
+    dev = rows.X.device
+    n = len(inits)
+    qscale = rows.fixed_point(comm)
+    a64 = rows.a_host.astype(np.float64)
+    b64 = rows.b_host.astype(np.float64)
+    fits = [_FitState(rows, c, dev) for c in inits]
+    ks = [fs.k for fs in fits]
+    rls = [N.query("mw_lloyd_rec_len", k, F) for k in ks]
+    roff = np.concatenate([[0], np.cumsum(rls)]).astype(np.int64)
+    out_all = torch.zeros(int(roff[-1]), dtype=torch.float64, device=dev)
+    outs = [out_all[roff[g]:roff[g + 1]] for g in range(n)]
+    plen = [k * F + 2 * k for k in ks]  # per fit: centers | drift | half_sep (fp32)
+    poff = np.concatenate([[0], np.cumsum(plen)]).astype(np.int64)
+    par = torch.empty(int(poff[-1]), dtype=torch.float32, device=dev)
+    host_par = np.zeros(int(poff[-1]), dtype=np.float32)
+    st = D.stream()
+
+    def upload(sel):
+        for g in sel:
+            fs = fits[g]
+            k = fs.k
+            c32 = fs.centers.astype(np.float32)
+            drift, dmax, half = _bound_tables(c32, fs.prev32)
+            fs.prev32, fs.drift_max = c32, dmax
+            o = int(poff[g])
+            host_par[o:o + k * F] = c32.ravel()
+            host_par[o + k * F:o + k * F + k] = drift
+            host_par[o + k * F + k:o + k * F + 2 * k] = half
+        D.h2d_into(par, host_par)
+
+    def run(sel, mode, kind_of):
+        by_kind = {}
+        for g in sel:
+            by_kind.setdefault(kind_of(g), []).append(g)
+        for kind, gs in sorted(by_kind.items()):
+            for i in range(0, len(gs), 24):
+                _launch_pass(rows, [(g, fits[g]) for g in gs[i:i + 24]], mode, kind, par, poff,
+                             outs, st)
+        comm.all_reduce_(out_all)
+        return D.d2h(out_all)
+
+    first = 3 if os.environ.get("MW_LLOYD_FIRST_ATOMIC") == "1" else KIND_FIRST
+
+    def kind_of(g):
+        h = fits[g].history
+        if not h:
+            return first
+        return KIND_TILE if h[-1][1] > QUEUE_BELOW * S_glob else KIND_QUEUE
+
+    S_glob = S
+    if comm.sharded():
+        S_glob = int(comm.all_gather_np(np.array([S], dtype=np.int64))[:, 0].sum())
+
+    for it in range(max_iter):
+        active = [g for g in range(n) if not fits[g].done]
+        if not active:
+            break
+        upload(active)
+        rec_all = run(active, 0, kind_of)
+        for g in active:
+            fs = fits[g]
+            sums, weight, changed = fs.add(rec_all[roff[g]:roff[g + 1]], F, qscale, a64, b64)
+            centers_new = sums.copy()
+            _relocate_empty(rows, fs.labels, fs.centers, centers_new, weight, comm)
+            _average_centers(centers_new, weight)
+            shift = np.sqrt(((centers_new - fs.centers) ** 2).sum(axis=1))
+            fs.centers = centers_new
+            fs.n_iter = it + 1
+            if verbose:
+                print(f"Iteration {it}: {int(changed)} labels changed.")
+            if changed == 0:
+                fs.strict = fs.done = True
+                if verbose:
+                    print(f"Converged at iteration {it}: strict convergence.")
+            elif (shift ** 2).sum() <= tol:
+                fs.done = True
+                if verbose:
+                    print(f"Converged at iteration {it}: center shift within tolerance {tol}.")
+            if fs.done:
+                out_all[roff[g]:roff[g + 1]].zero_()
+    for fs in fits:
+        fs.n_iter = fs.n_iter if fs.done else max_iter
+    # final pass: the extra E-step when not strictly converged, and inertia,
+    # each fit in a fixed point from a bound on any row's squared distance
+    xs = np.abs(a64) * rows.xmax.astype(np.float64) + np.abs(b64)
+    xnorm = float(np.sqrt((xs ** 2).sum()))
+    for fs in fits:
+        cmax = float(np.sqrt((fs.centers ** 2).sum(1)).max())
+        fs.iexp = _exp_below((xnorm + cmax) ** 2 * 1.01)
+    upload(list(range(n)))
+    for mode in (1, 2):
+        sel = [g for g in range(n) if (2 if fits[g].strict else 1) == mode]
+        for i in range(0, len(sel), 24):
+            _launch_pass(rows, [(g, fits[g]) for g in sel[i:i + 24]], mode, KIND_FIRST, par, poff,
+                         outs, st)
+    comm.all_reduce_(out_all)
+    rec_all = D.d2h(out_all)
+    res = []
+    for g, fs in enumerate(fits):
+        tail = rec_all[roff[g + 1] - 4:roff[g + 1]]
+        inertia = float((tail[2] * 4294967296.0 + tail[3]) * 2.0 ** -fs.iexp)
+        res.append((fs.labels, inertia, fs.centers, fs.n_iter))
+    LAST_STATS["recomputed"] = [fs.recomputed for fs in fits]
+    LAST_STATS["history"] = [fs.history for fs in fits]
+    return res
+
+
+LAST_STATS = {}  # diagnostics of the last lloyd_fits call (rows recomputed per fit)
+
+
 def lloyd_device(rows: DeviceRows, centers_init: np.ndarray, max_iter=300, tol=0.0, verbose=False,
                  comm=LOCAL):
     """``_kmeans_single_lloyd`` on device.  Returns (labels u8 tensor, inertia,
     centers fp64, n_iter)."""
-    S, F = rows.S, rows.F
-    k = centers_init.shape[0]
-    dev = rows.X.device
-    labels = torch.full((S,), 255, dtype=torch.uint8, device=dev)  # = -1: nothing assigned
-    ws = D.WS.get("lloyd", N.query("mw_lloyd_ws_bytes", S, k, F))
-    rl = k * F + k + 2
-    out = torch.empty(rl, dtype=torch.float64, device=dev)
-    c32 = torch.empty((k, F), dtype=torch.float32, device=dev)
-    centers = np.array(centers_init, dtype=np.float64)
-    strict = False
-    st = D.stream()
-
-    def step(mode):
-        D.h2d_into(c32, centers.astype(np.float32))
-        with profiling.timed(f"lloyd_step_mode{mode}", S * (F * 4 + (2 if mode < 2 else 1))):
-            N.call("mw_lloyd_step", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(c32), k,
-                   D.P(labels), mode, D.P(ws), st)
-        N.call("mw_lloyd_reduce", D.P(ws), S, k, F, D.P(out), st)
-        comm.all_reduce_(out)
-        return D.d2h(out)
-
-    i = 0
-    for i in range(max_iter):
-        rec = step(0)
-        centers_new = rec[:k * F].reshape(k, F).copy()
-        weight = rec[k * F:k * F + k].copy()
-        changed = rec[k * F + k]
-        _relocate_empty(rows, labels, centers, centers_new, weight, comm)
-        _average_centers(centers_new, weight)
-        shift = np.sqrt(((centers_new - centers) ** 2).sum(axis=1))
-        centers = centers_new
-        if verbose:
-            print(f"Iteration {i}: {int(changed)} labels changed.")
-        if changed == 0:
-            strict = True
-            if verbose:
-                print(f"Converged at iteration {i}: strict convergence.")
-            break
-        if (shift ** 2).sum() <= tol:
-            if verbose:
-                print(f"Converged at iteration {i}: center shift within tolerance {tol}.")
-            break
-    rec = step(2 if strict else 1)
-    inertia = float(rec[k * F + k + 1])
-    return labels, inertia, centers, i + 1
+    return lloyd_fits(rows, [centers_init], max_iter, tol, verbose, comm)[0]
 
 
-def _mb_class(k: int) -> int:
-    return 1 if k <= 16 else 2 if k <= 32 else 4
+def lloyd_step_device(rows: DeviceRows, centers: np.ndarray, comm=LOCAL):
+    """One Lloyd iteration from ``centers`` with no prior labels
+    (lloyd_iter_chunked_dense): (labels u8 tensor, per-cluster sums of the
+    scaled rows fp64, cluster sizes)."""
+    qscale = rows.fixed_point(comm)
+    fs = _FitState(rows, centers, rows.X.device)
+    F = rows.F
+    rl = N.query("mw_lloyd_rec_len", fs.k, F)
+    out = torch.zeros(rl, dtype=torch.float64, device=rows.X.device)
+    c32 = fs.centers.astype(np.float32)
+    drift, dmax, half = _bound_tables(c32, None)
+    fs.drift_max = dmax
+    par = D.h2d(np.concatenate([c32.ravel(), drift, half]).astype(np.float32), rows.X.device)
+    _launch_pass(rows, [(0, fs)], 0, KIND_FIRST, par, np.zeros(1, dtype=np.int64), [out], D.stream())
+    comm.all_reduce_(out)
+    sums, weight, _ = fs.add(D.d2h(out), F, qscale, rows.a_host.astype(np.float64),
+                             rows.b_host.astype(np.float64))
+    return fs.labels, sums, weight
 
 
 def lloyd_device_multi(rows: DeviceRows, inits, max_iter=300, tol=0.0, comm=LOCAL):
-    """``lloyd_device`` for several independent fits over the same rows, run in
-    lockstep: every iteration is ONE pass over the rows for all the fits
-    still running (``mw_lloyd_step_multi``, fits of one M-step class per
-    launch), one all-reduce and one device-to-host copy of all their records.
-    Each fit's arithmetic is the single-fit kernel's, so every fit returns
-    exactly what ``lloyd_device`` returns for it.  Returns a list of
-    (labels u8 tensor, inertia, centers fp64, n_iter)."""
-    S, F = rows.S, rows.F
-    dev = rows.X.device
-    n = len(inits)
-    ks = [int(np.asarray(c).shape[0]) for c in inits]
-    rls = [k * F + k + 2 for k in ks]
-    roff = np.concatenate([[0], np.cumsum(rls)]).astype(np.int64)
-    coff = np.concatenate([[0], np.cumsum([k * F for k in ks])]).astype(np.int64)
-    out_all = torch.zeros(int(roff[-1]), dtype=torch.float64, device=dev)
-    c32_all = torch.empty(int(coff[-1]), dtype=torch.float32, device=dev)
-    host_c = np.zeros(int(coff[-1]), dtype=np.float32)
-    labels = [torch.full((S,), 255, dtype=torch.uint8, device=dev) for _ in range(n)]
-    wss = [torch.empty(N.query("mw_lloyd_ws_bytes", S, k, F), dtype=torch.uint8, device=dev)
-           for k in ks]
-    centers = [np.array(c, dtype=np.float64) for c in inits]
-    done = [False] * n
-    strict = [False] * n
-    n_iter = [max_iter] * n
-    st = D.stream()
-    import ctypes
-
-    def launch(group, mode):
-        m = len(group)
-        P = ctypes.c_void_p * m
-        cp = P(*[D.P(c32_all) + int(coff[g]) * 4 for g in group])
-        kk = (ctypes.c_int * m)(*[ks[g] for g in group])
-        lp = P(*[D.P(labels[g]) for g in group])
-        wp = P(*[D.P(wss[g]) for g in group])
-        op = P(*[D.P(out_all) + int(roff[g]) * 8 for g in group])
-        nbytes = sum(S * (F * 4 + (2 if mode < 2 else 1)) for _ in group)
-        with profiling.timed(f"lloyd_multi_mode{mode}", nbytes):
-            N.call("mw_lloyd_step_multi", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), m,
-                   ctypes.addressof(cp), ctypes.addressof(kk), ctypes.addressof(lp), mode,
-                   ctypes.addressof(wp), ctypes.addressof(op), st)
-
-    def run(sel, mode_of):
-        """One pass for the fits in ``sel``; returns the host records."""
-        for g in sel:
-            host_c[coff[g]:coff[g + 1]] = centers[g].ravel()
-        D.h2d_into(c32_all, host_c)
-        classes = {}
-        for g in sel:
-            classes.setdefault((mode_of(g), _mb_class(ks[g])), []).append(g)
-        for (mode, _), group in sorted(classes.items()):
-            for i in range(0, len(group), 24):
-                launch(group[i:i + 24], mode)
-        comm.all_reduce_(out_all)
-        return D.d2h(out_all)
-
-    for it in range(max_iter):
-        active = [g for g in range(n) if not done[g]]
-        if not active:
-            break
-        rec_all = run(active, lambda g: 0)
-        for g in active:
-            k = ks[g]
-            rec = rec_all[roff[g]:roff[g + 1]]
-            centers_new = rec[:k * F].reshape(k, F).copy()
-            weight = rec[k * F:k * F + k].copy()
-            changed = rec[k * F + k]
-            _relocate_empty(rows, labels[g], centers[g], centers_new, weight, comm)
-            _average_centers(centers_new, weight)
-            shift = np.sqrt(((centers_new - centers[g]) ** 2).sum(axis=1))
-            centers[g] = centers_new
-            if changed == 0:
-                strict[g], done[g], n_iter[g] = True, True, it + 1
-            elif (shift ** 2).sum() <= tol:
-                done[g], n_iter[g] = True, it + 1
-    rec_all = run(list(range(n)), lambda g: 2 if strict[g] else 1)
-    return [(labels[g], float(rec_all[roff[g] + ks[g] * F + ks[g] + 1]), centers[g], n_iter[g])
-            for g in range(n)]
+    """``lloyd_device`` for several fits, batched (see lloyd_fits)."""
+    return lloyd_fits(rows, inits, max_iter, tol, False, comm)
 
 
 def fit_many(rows: DeviceRows, k_values, random_state=None, comm=None, **kw):
     """``KMeans(n_clusters=k, random_state=random_state, **kw).fit(rows)`` for
-    every k, with the Lloyd iterations of all fits batched
-    (``lloyd_device_multi``); k-means++ seeding per fit as in ``KMeans.fit``.
-    Returns the fitted estimators (bitwise equal to separate fits)."""
+    every k, with the Lloyd iterations of all fits batched (``lloyd_fits``).
+
+    k-means++ with an int seed draws from a fresh RandomState(seed) per fit:
+    the first center and each step's n_local_trials = 2 + int(ln k) uniforms
+    (_kmeans.py:225-243) are the same for every k with the same
+    n_local_trials, so the centers of such a k are a prefix of the largest k's
+    (groups {2}, {3..7}, {8..20} for k = 2..20).  One seeding per group serves
+    all its k.  Returns the fitted estimators (bitwise equal to separate
+    fits)."""
     comm = LOCAL if comm is None else comm
-    models, inits = [], []
+    models = []
     for k in k_values:
         km = KMeans(n_clusters=int(k), random_state=random_state, **kw)
         km._check(rows.S)
         if km.n_init not in ("auto", 1) or not isinstance(km.init, str) or km.init != "k-means++":
             raise NotImplementedError("fit_many: k-means++ with a single init only")
         km._tol = float(np.mean(rows.feature_var()) * km.tol) if km.tol else 0.0
-        seeded = isinstance(km.random_state, (int, np.integer)) and not isinstance(km.random_state, bool)
-        c0, km.init_indices_ = km._kpp(rows, km.random_state if seeded else
-                                       as_random_state(km.random_state), comm)
         models.append(km)
-        inits.append(c0)
+    seeded = isinstance(random_state, (int, np.integer)) and not isinstance(random_state, bool)
+    inits = [None] * len(models)
+    if seeded:
+        groups = {}
+        for i, km in enumerate(models):
+            groups.setdefault(2 + int(np.log(km.n_clusters)), []).append(i)
+        for T, idx in groups.items():
+            kmax = max(models[i].n_clusters for i in idx)
+            big = KMeans(n_clusters=kmax, random_state=random_state)
+            c0, ii = big._kpp(rows, random_state, comm)
+            for i in idx:
+                k = models[i].n_clusters
+                inits[i], models[i].init_indices_ = c0[:k].copy(), ii[:k].copy()
+    else:
+        for i, km in enumerate(models):
+            inits[i], km.init_indices_ = km._kpp(rows, as_random_state(km.random_state), comm)
     tols = {km._tol for km in models}
     max_iters = {km.max_iter for km in models}
     assert len(tols) == 1 and len(max_iters) == 1
-    res = lloyd_device_multi(rows, inits, max_iters.pop(), tols.pop(), comm)
+    res = lloyd_fits(rows, inits, max_iters.pop(), tols.pop(), False, comm)
     for km, (labels, inertia, centers, n_iter) in zip(models, res):
         km._set_fitted(rows, labels, inertia, centers, n_iter)
     return models

@@ -153,21 +153,51 @@ def test_kmeans_plusplus_indices(gpu, golden):
 
 
 def test_single_lloyd_step(gpu, golden):
-    from milwrm_amd.kmeans import DeviceRows, lloyd_device
+    """One Lloyd iteration from the golden centers (lloyd_iter_chunked_dense):
+    labels bitwise (outside reference near-ties), cluster sizes exactly,
+    averaged centers and center shift against the reference's step."""
+    from milwrm_amd.kmeans import DeviceRows, lloyd_step_device
 
     g = golden("mxif_small")
     X = g["cluster_data"]
     Xc = X - X.mean(axis=0)
+    cin = g["lloyd1_centers_in"]
     rows = DeviceRows.from_host(Xc)
-    labels, _, centers, n_iter = lloyd_device(rows, g["lloyd1_centers_in"], max_iter=1, tol=0.0)
-    lab = labels.cpu().numpy()
-    # the extra E-step after a non-converged single iteration relabels with the
-    # new centers; compare the step itself through the oracle instead
-    ref_lab, ref_c, ref_w, _ = O.lloyd_iter(Xc, g["lloyd1_centers_in"])
-    np.testing.assert_array_equal(ref_lab, g["lloyd1_labels"])
+    lab, sums, w = lloyd_step_device(rows, cin)
+    lab = lab.cpu().numpy().astype(np.int32)
+    d = np.sort(((Xc[:, None, :] - cin[None]) ** 2).sum(-1), axis=1)
+    near = (d[:, 1] - d[:, 0]) / d[:, 1] < TAU
+    assert not np.any((lab != g["lloyd1_labels"]) & ~near)
+    if not near.any():
+        np.testing.assert_array_equal(lab, g["lloyd1_labels"])
+        np.testing.assert_array_equal(w, g["lloyd1_weights"])
+    assert np.all(w > 0)
+    centers = sums / w[:, None]
     np.testing.assert_allclose(centers, g["lloyd1_centers_out"], rtol=RTOL, atol=1e-6)
-    lab2, _, _, _ = O.lloyd_iter(Xc, centers, update_centers=False)
-    assert np.mean(lab == lab2) > 0.999
+    shift = np.sqrt(((centers - cin) ** 2).sum(axis=1))
+    np.testing.assert_allclose(shift, g["lloyd1_shift"], rtol=1e-3, atol=1e-6)
+
+
+def test_bounded_lloyd_labels_are_argmin(gpu):
+    """The bound-pruned E-step (rows whose bounds prove their label skip the
+    distances) gives every row the label of the plain fp32 argmin: after a
+    fit, one full E-step (mode 1) with the final centers changes nothing on a
+    strictly converged fit, and the labels equal a brute-force argmin."""
+    from milwrm_amd.kmeans import DeviceRows, KMeans, LAST_STATS
+
+    rng = np.random.default_rng(3)
+    X = np.concatenate([rng.normal(m, 1.0, size=(4000, 12)) for m in (-2, 0, 2, 4)])
+    X = (X - X.mean(0)) / X.std(0)
+    rows = DeviceRows.from_host(X)
+    km = KMeans(n_clusters=6, random_state=18, tol=0.0).fit(rows)
+    assert sum(LAST_STATS["recomputed"]) < km.n_iter_ * X.shape[0]  # the bounds pruned work
+    c32 = km.cluster_centers_.astype(np.float32).astype(np.float64)
+    x32 = X.astype(np.float32).astype(np.float64)
+    d = ((x32[:, None, :] - c32[None]) ** 2).sum(-1)
+    ds = np.sort(d, axis=1)
+    near = (ds[:, 1] - ds[:, 0]) / ds[:, 1] < TAU
+    lab = km.labels_
+    assert not np.any((lab != np.argmin(d, axis=1)) & ~near)
 
 
 def test_kmeans_fit_matches_reference(gpu, golden):
@@ -215,7 +245,7 @@ def _sweep_rows(golden, which):
 @pytest.mark.parametrize("which", ["mxif_small", "hard256", "noise"])
 def test_batched_sweep_equals_separate_fits(gpu, golden, which):
     """find_optimal_k's batched Lloyd (all k in one pass per iteration,
-    mw_lloyd_step_multi) returns exactly what separate KMeans fits return:
+    mw_lloyd_pass with every running fit) returns exactly what separate KMeans fits return:
     same k-means++ indices, n_iter, labels, and bitwise equal centers and
     inertia for k = 2..20 (both M-step classes, k <= 16 and 17..20)."""
     from milwrm_amd.kmeans import KMeans, fit_many

@@ -1,6 +1,7 @@
 """Blur-only timing on one synthetic 30-channel uint16 slide: kernel time per
-launch (HIP events on the launch stream) for several band widths
-(MW_BLUR_BW override), plus a bitwise cross-check between the variants."""
+launch (HIP events on the launch stream) for several band geometries
+(env overrides, e.g. MW_BLUR_BH=256 MW_BLUR_BT=3), plus a bitwise cross-check
+between the variants."""
 import os
 import sys
 
@@ -15,11 +16,13 @@ torch.cuda.set_device(0)
 raw, mask = D.synth_slide(size, size, C, seed=7, mode="hard")
 inv = torch.rand(C, device="cuda", dtype=torch.float32) * 1e-3 + 1e-4
 ref = None
-for bw in ["", "64", "32", "16"]:
-    if bw:
-        os.environ["MW_BLUR_BW"] = bw
-    else:
-        os.environ.pop("MW_BLUR_BW", None)
+variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["", "MW_BLUR_BH=256"]
+for bw in variants:
+    for kv in ("MW_BLUR_BH", "MW_BLUR_XCD", "MW_BLUR_BT"):
+        os.environ.pop(kv, None)
+    for kv in filter(None, bw.split(";")):
+        k, v = kv.split("=")
+        os.environ[k] = v
     out = D.blur(raw, 2.0, inv_mean=inv)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -34,5 +37,5 @@ for bw in ["", "64", "32", "16"]:
     same = None if ref is None else bool(torch.equal(out, ref))
     if ref is None:
         ref = out.clone()
-    print(f"BW={bw or 'default'}: {ms:.3f} ms/launch, {gb / ms:.0f} GB/s algorithmic, same={same}",
+    print(f"BW={bw or 'default'}: {ms:.3f} ms/launch, {gb / ms * 1e3:.0f} GB/s algorithmic, same={same}",
           flush=True)

@@ -1,5 +1,5 @@
 """find_optimal_k (k = 2..20, MILWRM.py:659-704) on one synthetic slide:
-batched Lloyd (all k per pass, mw_lloyd_step_multi) against one fit after
+batched Lloyd (all k per pass, mw_lloyd_pass) against one fit after
 another (MW_SWEEP_BATCH=0).  Rows prepared once (untimed); each sweep timed
 with a device synchronisation on both sides.  Prints one JSON line.
 
@@ -62,6 +62,9 @@ def main():
         out[name] = {"s": min(ts), "best_k": int(lab.k),
                      "kernels_ms": {k: round(v["total_ms"], 2) for k, v in sorted(prof.items())}}
         out[name + "_curve"] = [float(x) for x in curve]
+        if name == "batched":
+            from milwrm_amd.kmeans import LAST_STATS
+            out["rows_recomputed_per_k"] = LAST_STATS.get("recomputed")
     out["identical_curve"] = bool(np.array_equal(out["batched_curve"], out["sequential_curve"]))
     out["speedup"] = out["sequential"]["s"] / out["batched"]["s"]
     print(json.dumps(out), flush=True)
