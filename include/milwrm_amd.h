@@ -287,16 +287,27 @@ int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom,
 
 /* ---- clustering QC statistics ------------------------------------------------
  * Replaces the per-domain loops of estimate_percentage_variance_mxif
- * (MILWRM.py:280-333, dc/dm sums) and estimate_mse_mxif (MILWRM.py:453-515).
- * Over n_pix HWC fp32 pixels, x' = x[feat[f]]*a[f] + b[f] (fp64):
- * d_out (fp64, M = k*F + 2F + k) = [sum over label==d of (x'_f - c_df)^2 (k x F)
- * | sum x'_f (F) | sum x'_f^2 (F, over every pixel) | pixel count per label (k)].
- * Labels outside [0, k) (masked / NaN tissue_ID → -1) add to the sums only.
- * 1 <= k <= 20, 1 <= F <= 256; deterministic (fixed fold order). */
+ * (MILWRM.py:280-333, dc/dm sums), estimate_mse_mxif (MILWRM.py:453-515) and
+ * their ST twins estimate_percentage_variance_st / estimate_mse_st
+ * (MILWRM.py:518-554, 601-644; rows as a 1-pixel-wide image).
+ * Over n_pix HWC fp32 pixels, x' = x[feat[f]]*a[f] + b[f], y = x' - pivot[f] (fp64):
+ * d_out (fp64, M = k*F + 2F + k) = [sum over label == d0+d of (x'_f - c_df)^2 (k x F)
+ * | sum y_f (F) | sum y_f^2 (F, over every pixel) | pixel count per label (k)].
+ * Labels outside [d0, d0+k) (other domains; masked / NaN tissue_ID → -1) add to
+ * the sums only.  1 <= k <= 20 domains per call (more: several calls with d0 =
+ * 0, 20, 40, ...), 1 <= F <= 256; deterministic (fixed fold order). */
 size_t mw_domain_sse_ws_bytes(int64_t n_pix, int k, int F);
 int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
-                  const double* d_b, const double* d_centers, int k, const int8_t* d_label,
-                  int64_t n_pix, double* d_out, void* d_ws, void* stream);
+                  const double* d_b, const double* d_pivot, const double* d_centers, int k, int d0,
+                  const int8_t* d_label, int64_t n_pix, double* d_out, void* d_ws, void* stream);
+
+/* ---- ST feature blur (blur_features_st, ST.py:25-77) --------------------------
+ * out[i, f] = mean of X[j, f] over j in (nonzero columns of row i of the CSR
+ * spatial graph, in column order) + [i] (a self-loop therefore counts twice,
+ * as in the reference), NaN entries skipped (pandas mean); NaN if none.
+ * CSR: d_indptr (n+1, int64), d_indices (int32); X, out: n x F fp64 row-major. */
+int mw_neighbor_mean(const int64_t* d_indptr, const int32_t* d_indices, int64_t n, const double* d_X,
+                     int F, double* d_out, void* stream);
 
 /* ---- synthetic slide generator (benchmark input; SURVEY §8d shape) ----------
  * uint16 HWC + uint8 mask: Voronoi domains (seeds given), per-domain channel

@@ -22,7 +22,8 @@ import pandas as pd
 import torch
 
 from . import device as D
-from .assign import assign_image, assign_rows, blur_assign_image, domain_means, domain_sse_image
+from .assign import (assign_image, assign_rows, blur_assign_image, dm_total, domain_means,
+                     domain_sse_image, domain_sse_rows)
 from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
@@ -148,17 +149,17 @@ def _domain_stats(image, use_path, scaler, centroids, features, tissue_ID):
         image = img.from_npz(image + ".npz")
     feats = image._features(features)
     mu, inv = scaler.affine()
-    src = D.as_float32(image._materialize())
+    # a deferred-blur slide is blurred into a temporary for this pass only
+    src = image._blurred_f32()
     return domain_sse_image(src, feats, mu, inv, np.asarray(centroids, dtype=np.float64),
                             tissue_ID)
 
 
 def estimate_percentage_variance_mxif(image, use_path, scaler, centroids, features, tissue_ID):
     """MILWRM.py:280-333: 100 * sum over domains of (x' - c)^2 / sum over the
-    whole slide of (x' - mean(x'))^2, from one ``mw_domain_sse`` pass."""
+    whole slide of (x' - mean(x'))^2, from ``mw_domain_sse`` passes."""
     s = _domain_stats(image, use_path, scaler, centroids, features, tissue_ID)
-    dm = float(np.sum(s["sumsq"] - s["sum"] * s["sum"] / s["n"]))
-    return float(np.sum(s["sse"])) / dm * 100
+    return np.float64(np.sum(s["sse"])) / dm_total(s) * 100
 
 
 def estimate_mse_mxif(images, use_path, tissue_IDs, scaler, centroids, features, k):
@@ -171,6 +172,40 @@ def estimate_mse_mxif(images, use_path, tissue_IDs, scaler, centroids, features,
         cnt = s["count"][:, None]
         mse_temp.append(np.where(cnt > 0, s["sse"] / np.maximum(cnt, 1), 0.0))
     return {i: [m[i] for m in mse_temp] for i in range(k)} if len(images) else {}
+
+
+def _st_labels(adata) -> np.ndarray:
+    t = adata.obs["tissue_ID"]
+    v = np.asarray(t.astype(float) if hasattr(t, "astype") else t, dtype=np.float64)
+    return np.where(np.isfinite(v), v, -1).astype(np.int64)
+
+
+def estimate_percentage_variance_st(sub_cluster_data, adata, centroids):
+    """MILWRM.py:518-554: the spots of one section, their tissue_IDs and the
+    centroids -> 100 * sum of (x - c_id)^2 / sum of (x - mean(x))^2 (one
+    ``mw_domain_sse`` pass over the section's rows)."""
+    X = np.asarray(sub_cluster_data, dtype=np.float64)
+    s = domain_sse_rows(X, np.asarray(centroids, dtype=np.float64), _st_labels(adata))
+    return np.float64(np.sum(s["sse"])) / dm_total(s) * 100
+
+
+def estimate_mse_st(cluster_data, adatas, centroids, k):
+    """MILWRM.py:601-644: {domain: [per-feature MSE for each section]}.  The
+    reference slices section m's rows as cluster_data[n_obs(m-1):...] (its
+    ``i_slice = adata.n_obs``), so section m >= 1 reads rows from offset
+    n_obs of the previous section; kept as is."""
+    cluster_data = np.asarray(cluster_data, dtype=np.float64)
+    centroids = np.asarray(centroids, dtype=np.float64)
+    per = []
+    off = 0
+    for adata in adatas:
+        lab = _st_labels(adata)
+        rows = cluster_data[off:off + adata.n_obs]
+        s = domain_sse_rows(rows, centroids[:k], lab)
+        cnt = s["count"][:, None]
+        per.append(np.where(cnt > 0, s["sse"] / np.maximum(cnt, 1), 0.0))
+        off = adata.n_obs
+    return {i: [m[i] for m in per] for i in range(k)}
 
 
 def _assign_img(image: img, features, centers, scaler):
@@ -237,6 +272,22 @@ def _conf_to_host(conf: torch.Tensor) -> np.ndarray:
 
 # ---------------------------------------------------------------- classes
 
+def _stacked_bar(df, cmap, figsize, xlabel, save_to):
+    """The reference's proportion bar chart (matplotlib)."""
+    import matplotlib.pyplot as plt
+
+    ax = df.plot.bar(stacked=True, cmap=cmap, figsize=figsize)
+    ax.legend(loc="best", bbox_to_anchor=(1, 1))
+    ax.set_xlabel(xlabel)
+    ax.set_ylabel("tissue domain proportion")
+    ax.set_ylim((0, 1))
+    plt.tight_layout()
+    if save_to is not None:
+        ax.figure.savefig(save_to)
+        return None
+    return ax
+
+
 class tissue_labeler:
     """MILWRM.py:647-922 (plots out of scope)."""
 
@@ -300,8 +351,6 @@ class tissue_labeler:
     plot_percentage_variance_explained = _plot
     plot_mse_mxif = _plot
     plot_mse_st = _plot
-    plot_tissue_ID_proportions_mxif = _plot
-    plot_tissue_ID_proportions_st = _plot
     make_umap = _plot
     show_marker_overlay = _plot
     plot_gene_loadings = _plot
@@ -451,6 +500,32 @@ class mxif_labeler(tissue_labeler):
         self._labels_dev, self._conf_dev, self._dom_dev = labs, confs, doms
         self.tissue_IDs = _LazyHostList(labs, _labels_to_host)
 
+    def plot_tissue_ID_proportions_mxif(self, tID_labels=None, slide_labels=None, figsize=(5, 5),
+                                        cmap="tab20", save_to=None):
+        """MILWRM.py:2013-2073: per image, the share of the masked pixels in each
+        tissue domain (``self.tissue_ID_proportion``, domains x images), from
+        the label pass's per-domain pixel counts; then the stacked bar plot."""
+        k = int(self.k)
+        if getattr(self, "_dom_dev", None):
+            doms = D.d2h(torch.stack(self._dom_dev))
+            counts = doms[:, k:2 * k].T  # domains x images
+        else:
+            counts = np.array([[np.sum(np.asarray(t) == j) for t in self.tissue_IDs]
+                               for j in range(k)], dtype=np.float64)
+        df_count = pd.DataFrame(counts.astype(np.int64), index=range(k),
+                                columns=range(counts.shape[1]))
+        df_count = df_count / df_count.sum()
+        if tID_labels:
+            assert len(tID_labels) == df_count.shape[1], \
+                "Length of given tissue domain labels does not match number of tissue domains!"
+            df_count.columns = tID_labels
+        if slide_labels:
+            assert len(slide_labels) == df_count.shape[0], \
+                "Length of given slide labels does not match number of slides!"
+            df_count.index = slide_labels
+        self.tissue_ID_proportion = df_count
+        return _stacked_bar(df_count.T, cmap, figsize, "images", save_to)
+
     def confidence_score_images(self):
         """MILWRM.py:1868-1900 from the fused pass: confidence_IDs and the
         images x domains DataFrame of mean confidences."""
@@ -512,6 +587,26 @@ class st_labeler(tissue_labeler):
             self.adatas[i].obs["tissue_ID"] = self.adatas[i].obs["tissue_ID"].cat.set_categories(
                 np.unique(IDs))
             start += self.adatas[i].n_obs
+
+    def plot_tissue_ID_proportions_st(self, tID_labels=None, slide_labels=None, figsize=(5, 5),
+                                      cmap="tab20", save_to=None):
+        """MILWRM.py:1400-1452: per section, the share of spots in each tissue
+        domain (value counts of the fit labels), as a stacked bar plot."""
+        df_count = pd.DataFrame()
+        for adata in self.adatas:
+            df = adata.obs["tissue_ID"].value_counts(normalize=True, sort=False)
+            df_count = pd.concat([df_count, df], axis=1)
+        df_count = df_count.T.reset_index(drop=True)
+        if tID_labels:
+            assert len(tID_labels) == df_count.shape[1], \
+                "Length of given tissue domain labels does not match number of tissue domains!"
+            df_count.columns = tID_labels
+        if slide_labels:
+            assert len(slide_labels) == df_count.shape[0], \
+                "Length of given slide labels does not match number of slides!"
+            df_count.index = slide_labels
+        self.tissue_ID_proportion = df_count
+        return _stacked_bar(df_count, cmap, figsize, "slides", save_to)
 
     def confidence_score(self):
         """MILWRM.py:1091-1121."""

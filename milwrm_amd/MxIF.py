@@ -108,6 +108,23 @@ class img:
             self._host64 = None
         return self._device()
 
+    def _blurred_f32(self) -> torch.Tensor:
+        """The preprocessed slide as fp32 for a read-only pass.  A deferred
+        blur (D.defer_blur: the slide did not fit HBM beside its blurred copy)
+        is computed into a temporary that is NOT kept: the img keeps its raw
+        slide and the fused epilogues stay in use."""
+        if self._pending_blur is None:
+            return D.as_float32(self._materialize())
+        sigma, truncate = self._pending_blur
+        inv, p = self._pending
+        src = self._device()
+        need = src.numel() * 4
+        free, _ = torch.cuda.mem_get_info()
+        if need > free:
+            raise MemoryError(f"this pass needs the blurred slide ({need / 2**30:.1f} GiB fp32) and "
+                              f"only {free / 2**30:.1f} GiB of HBM are free")
+        return D.blur(src, sigma, inv_mean=inv, pseudoval=p, truncate=truncate)
+
     def _set_device(self, t: torch.Tensor):
         self._dev = t
         self._host64 = None
@@ -391,8 +408,10 @@ class img:
 
     def create_tissue_mask(self, features=None, fract=0.2):
         """MxIF.py:543-589 on the device kernels: log-normalise (global channel
-        means), Gaussian sigma=2, subsample, KMeans(2, random_state=18) on the
-        UNscaled samples, predict every pixel, background flip."""
+        means), Gaussian sigma=2, subsample ``features``, KMeans(2,
+        random_state=18) on the UNscaled samples, predict every pixel on ALL
+        channels (as the reference's ``kmeans.predict(image_ar_reshape)``, so a
+        feature subset raises sklearn's feature-count error), background flip."""
         from .assign import assign_image
         from .kmeans import DeviceRows, KMeans
 
@@ -406,9 +425,11 @@ class img:
         F = X.shape[1]
         var = stats[1 + F:] / stats[0]
         km = KMeans(n_clusters=2, random_state=18).fit(DeviceRows(X, feature_var=var))
-        feats = cp._features(features)
-        lab, _, _ = assign_image(D.as_float32(cp._materialize()), feats, np.zeros(F), np.ones(F), km.cluster_centers_,
-                                 cp._mask_device())
+        d = cp.n_ch
+        if d != F:
+            raise ValueError(f"X has {d} features, but KMeans is expecting {F} features as input.")
+        lab, _, _ = assign_image(D.as_float32(cp._materialize()), list(range(d)), np.zeros(F),
+                                 np.ones(F), km.cluster_centers_, cp._mask_device())
         tID = lab.cpu().numpy().astype(float)
         scores = km.cluster_centers_
         z = (scores - scores.mean()) / scores.std()

@@ -1,16 +1,18 @@
 """ST-side plumbing of MILWRM (ST.py).  Only ``blur_features_st`` is on the
-st_labeler path; it is a tiny sparse neighbour mean over ~10^3-10^4 spots,
-kept on the host (scipy.sparse), outside the GPU hot path.
-The Visium image utilities are out of scope."""
+st_labeler path: the neighbour mean over the spatial graph runs on the device
+(``mw_neighbor_mean``, a CSR sparse product).  The Visium image utilities are
+out of scope."""
 from __future__ import annotations
 
 import numpy as np
 import scipy.sparse as sp
+import torch
 
 
 def blur_features_st(adata, tmp, spatial_graph_key=None, n_rings=1):
-    """ST.py:25-77: each spot's features averaged with its non-zero spatial
-    neighbours (a self-loop in the graph counts twice, as in the reference)."""
+    """ST.py:25-77: each spot's features averaged (NaN skipped, as pandas'
+    mean) with its non-zero spatial neighbours; a self-loop in the graph
+    counts twice, as in the reference."""
     if spatial_graph_key is not None:
         assert spatial_graph_key in adata.obsp.keys(), \
             "Spatial connectivities key '{}' not found.".format(spatial_graph_key)
@@ -23,15 +25,24 @@ def blur_features_st(adata, tmp, spatial_graph_key=None, n_rings=1):
         print("Computing spatial graph with {} hexagonal rings".format(n_rings))
         sq.gr.spatial_neighbors(adata, coord_type="grid", n_rings=n_rings)
         spatial_graph_key = "spatial_connectivities"
+    from . import _native as N
+    from . import device as D
+
     A = sp.csr_matrix(adata.obsp[spatial_graph_key])
-    A.eliminate_zeros()
-    A.data = np.ones_like(A.data, dtype=np.float64)
+    A.sum_duplicates()
+    A.eliminate_zeros()  # np.argwhere of the row: stored zeros are no neighbours
+    A.sort_indices()
     n = A.shape[0]
-    M = A + sp.identity(n, format="csr")
-    deg = np.asarray(A.getnnz(axis=1) + 1, dtype=np.float64)
     cols = tmp.columns
-    vals = tmp.loc[:, cols].values.astype(np.float64)
-    blurred = (M @ vals) / deg[:, None]
+    vals = np.ascontiguousarray(tmp.loc[:, cols].values, dtype=np.float64)
+    F = vals.shape[1]
+    dev = D.device()
+    ip = torch.from_numpy(A.indptr.astype(np.int64)).to(dev)
+    ix = torch.from_numpy(A.indices.astype(np.int32)).to(dev)
+    xv = torch.from_numpy(vals).to(dev)
+    out = torch.empty_like(xv)
+    N.call("mw_neighbor_mean", D.P(ip), D.P(ix), n, D.P(xv), F, D.P(out), D.stream())
+    blurred = D.d2h(out)
     tmp2 = tmp.copy()
     tmp2.loc[:, cols] = blurred
     adata.obs[[x for x in cols]] = tmp.loc[:, cols].values

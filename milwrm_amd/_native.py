@@ -69,7 +69,8 @@ _PROTOS = {
     "mw_assign_conf": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_reduce": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_domain_sse_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
-    "mw_domain_sse": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "mw_domain_sse": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "mw_neighbor_mean": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_col_stats_rows": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_sample_head_elems": (c_sz, [c_i64]),
     "mw_sample_map": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),

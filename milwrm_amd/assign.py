@@ -76,18 +76,22 @@ def blur_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: floa
 
 
 def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
-                     tissue_id) -> dict:
-    """Per-domain squared error and whole-slide scaled sums in one pass
-    (``mw_domain_sse``; the sums behind ``estimate_percentage_variance_mxif``
-    MILWRM.py:280-333 and ``estimate_mse_mxif`` MILWRM.py:453-515).
+                     tissue_id, pivot=None) -> dict:
+    """Per-domain squared error and whole-slide scaled sums (``mw_domain_sse``;
+    the sums behind ``estimate_percentage_variance_mxif`` MILWRM.py:280-333,
+    ``estimate_mse_mxif`` :453-515 and the ST twins :518-554, :601-644), one
+    pass per 20 domains.
 
     ``tissue_id``: H x W labels as the reference holds them (float, NaN outside
-    the mask) or an int8 device map with -1 outside the mask.  Returns fp64
-    host arrays: sse (k x F), sum (F), sumsq (F), count (k), n (pixels)."""
+    the mask) or an int8 device map with -1 outside the mask.  ``pivot``: the
+    shift of the whole-slide sums (default: the scaled features of the first
+    pixel, which keeps a near-constant feature free of cancellation).  Returns
+    fp64 host arrays: sse (k x F), sum / sumsq of x' - pivot (F), count (k),
+    n (pixels), pivot (F)."""
     H, W, C = img_f32.shape
     k, F = centers.shape
-    if not 1 <= k <= 20:
-        raise ValueError(f"domain statistics support 1 <= k <= 20 domains, got {k}")
+    if not 1 <= k <= 127:
+        raise ValueError(f"domain statistics support 1 <= k <= 127 domains, got {k}")
     img_f32 = img_f32.contiguous()
     feat = np.asarray(feat_idx, dtype=np.int32)
     feat = np.where(feat < 0, feat + C, feat).astype(np.int32)
@@ -103,21 +107,58 @@ def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarr
             raise ValueError(f"tissue_ID has {t.size} pixels, image has {n}")
         ok = np.isfinite(t) & (t >= 0) & (t < k) & (t == np.floor(t))
         lab = D.h2d(np.where(ok, t, -1).astype(np.int8), dev)
+    mu = np.asarray(mu, dtype=np.float64)
     inv = np.asarray(inv, dtype=np.float64)
+    if pivot is None:
+        x0 = D.d2h(img_f32.reshape(n, C)[0]).astype(np.float64)[feat]
+        pivot = x0 * inv - mu * inv
     a = D.h2d(inv, dev)
-    b = D.h2d(-np.asarray(mu, dtype=np.float64) * inv, dev)
-    c64 = D.h2d(np.ascontiguousarray(centers, dtype=np.float64), dev)
+    b = D.h2d(-mu * inv, dev)
+    pv = D.h2d(np.asarray(pivot, dtype=np.float64), dev)
     feat_d = D.h2d(feat, dev)
-    M = k * F + 2 * F + k
-    out = torch.empty(M, dtype=torch.float64, device=dev)
-    ws = D.WS.get("domain_sse", N.query("mw_domain_sse_ws_bytes", n, k, F))
+    cen = np.ascontiguousarray(centers, dtype=np.float64)
     st = D.stream()
-    with profiling.timed("domain_sse", n * (C * 4 + 1)):
-        N.call("mw_domain_sse", D.P(img_f32), C, D.P(feat_d), F, D.P(a), D.P(b), D.P(c64),
-               k, D.P(lab), n, D.P(out), D.P(ws), st)
-    o = out.cpu().numpy()
-    return {"sse": o[:k * F].reshape(k, F), "sum": o[k * F:k * F + F],
-            "sumsq": o[k * F + F:k * F + 2 * F], "count": o[k * F + 2 * F:], "n": n}
+    sse = np.zeros((k, F))
+    count = np.zeros(k)
+    sums = None
+    for d0 in range(0, k, 20):
+        kc = min(20, k - d0)
+        c64 = D.h2d(cen[d0:d0 + kc], dev)
+        M = kc * F + 2 * F + kc
+        out = torch.empty(M, dtype=torch.float64, device=dev)
+        ws = D.WS.get("domain_sse", N.query("mw_domain_sse_ws_bytes", n, kc, F))
+        with profiling.timed("domain_sse", n * (C * 4 + 1)):
+            N.call("mw_domain_sse", D.P(img_f32), C, D.P(feat_d), F, D.P(a), D.P(b), D.P(pv),
+                   D.P(c64), kc, d0, D.P(lab), n, D.P(out), D.P(ws), st)
+        o = D.d2h(out)
+        sse[d0:d0 + kc] = o[:kc * F].reshape(kc, F)
+        count[d0:d0 + kc] = o[kc * F + 2 * F:]
+        if sums is None:
+            sums = (o[kc * F:kc * F + F], o[kc * F + F:kc * F + 2 * F])
+    return {"sse": sse, "sum": sums[0], "sumsq": sums[1], "count": count, "n": n,
+            "pivot": np.asarray(pivot, dtype=np.float64)}
+
+
+def domain_sse_rows(X: np.ndarray, centers: np.ndarray, labels) -> dict:
+    """``domain_sse_image`` over host rows already in the centers' space (the
+    ST estimators' cluster_data): the rows travel as a 1-pixel-wide fp32
+    image, labels < 0 belong to no domain."""
+    X = np.asarray(X, dtype=np.float64)
+    S, F = X.shape
+    dev = D.device()
+    img = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32).reshape(S, 1, F)).to(dev)
+    lab = torch.from_numpy(np.asarray(labels, dtype=np.int64).clip(-1, 127).astype(np.int8)).to(dev)
+    x0 = X[0].astype(np.float32).astype(np.float64)
+    return domain_sse_image(img, np.arange(F), np.zeros(F), np.ones(F), centers, lab.reshape(S, 1),
+                            pivot=x0)
+
+
+def dm_total(s: dict) -> np.float64:
+    """sum over pixels and features of (x' - mean(x'))^2 from the shifted sums
+    (np.float64, so a zero denominator gives inf / nan as the reference's
+    numpy division does)."""
+    n = np.float64(s["n"])
+    return np.float64(np.sum(s["sumsq"] - s["sum"] * s["sum"] / n))
 
 
 def assign_rows(X: np.ndarray, centers: np.ndarray, mu=None, inv=None):

@@ -71,7 +71,8 @@ __device__ __forceinline__ float dist_one(const f2v (&x2)[FMAX / 2], const f2v* 
 // bytes of one wave's row tile (64 rows x FMAX floats)
 __host__ __device__ inline size_t lloyd_tile_bytes(int FMAX) { return (size_t)64 * FMAX * 4; }
 
-constexpr int kChunk = 4096;  // rows per bound-test chunk (sparse passes): queue of u16 offsets
+constexpr int kChunk = 4096;  // rows per bound-test chunk (kQueue passes): queue of u16 offsets
+static_assert(kChunk % 1024 == 0, "chunk = whole 4-wave x 256-row groups");
 
 // small per-block LDS state (size a multiple of 16 bytes)
 struct alignas(16) LloydSmall {
@@ -117,7 +118,7 @@ constexpr int kFirstAtomic = 3;  // kFirst with the sums by LDS atomics (A/B)
 //     passes where few rows are undecided.
 //   MODE 1: full E-step (labels updated) + inertia of the new labels
 //   MODE 2: inertia of the current labels
-template <int FMAX, int MODE, int KIND>
+template <int FMAX, int MODE, int KIND, int MBT>
 __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict__ X, int64_t S, int F,
                                                          const float* __restrict__ ga,
                                                          const float* __restrict__ gb,
@@ -247,39 +248,49 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
     for (int64_t c0 = lo; c0 < hi; c0 += kChunk) {
       const int clen = (int)min((int64_t)kChunk, hi - c0);
       // ---- phase 1: bound test, 4 consecutive rows per lane, queue the undecided ----
-      for (int base = wid * 256; base < clen; base += nw * 256) {
-        const int off0 = base + 4 * lane;
+      // (the wave's whole share of the chunk, kChunk / (4 waves * 256 rows) =
+      // 4 row groups, is loaded before any of it is used: 12 loads in flight)
+      constexpr int NI = kChunk / (4 * 256);
+      uint32_t lab4[NI];
+      f4v ub4[NI], lb4[NI];
+#pragma unroll
+      for (int it = 0; it < NI; ++it) {
+        const int off0 = (wid + it * nw) * 256 + 4 * lane;
         const int64_t r0 = c0 + off0;
-        uint32_t lab4;
-        f4v ub4, lb4;
-        if (off0 + 3 < clen && (r0 & 3) == 0) {
-          lab4 = *reinterpret_cast<const uint32_t*>(labels + r0);
-          ub4 = *reinterpret_cast<const f4v*>(ubuf + r0);
-          lb4 = *reinterpret_cast<const f4v*>(lbuf + r0);
+        if (off0 + 3 < clen) {  // r0 % 4 == 0: lo, c0 and off0 are multiples of 4
+          lab4[it] = *reinterpret_cast<const uint32_t*>(labels + r0);
+          ub4[it] = *reinterpret_cast<const f4v*>(ubuf + r0);
+          lb4[it] = *reinterpret_cast<const f4v*>(lbuf + r0);
         } else {
-          lab4 = 0xFFFFFFFFu;
+          lab4[it] = 0xFFFFFFFFu;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             if (off0 + i < clen) {
-              lab4 = (lab4 & ~(0xFFu << (8 * i))) | ((uint32_t)labels[r0 + i] << (8 * i));
-              ub4[i] = ubuf[r0 + i];
-              lb4[i] = lbuf[r0 + i];
+              lab4[it] = (lab4[it] & ~(0xFFu << (8 * i))) | ((uint32_t)labels[r0 + i] << (8 * i));
+              ub4[it][i] = ubuf[r0 + i];
+              lb4[it][i] = lbuf[r0 + i];
             }
           }
         }
+      }
+#pragma unroll
+      for (int it = 0; it < NI; ++it) {
+        const int off0 = (wid + it * nw) * 256 + 4 * lane;
+        if ((wid + it * nw) * 256 >= clen) break;  // wave-uniform
+        const int64_t r0 = c0 + off0;
         bool skip[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int lab_old = (lab4 >> (8 * i)) & 0xFF;
+          const int lab_old = (lab4[it] >> (8 * i)) & 0xFF;
           const int la = lab_old < k ? lab_old : 0;
-          const float ub = ub4[i] + s_drift[la];
-          const float lbv = lb4[i] - dmax;
+          const float ub = ub4[it][i] + s_drift[la];
+          const float lbv = lb4[it][i] - dmax;
           const float thr = fmaxf(lbv, s_half[la]);
           const bool valid = off0 + i < clen;
           const bool need = valid && (lab_old >= k || !(ub * (1.f + kEps) < thr));
           skip[i] = valid && !need;
-          ub4[i] = ub;
-          lb4[i] = lbv;
+          ub4[it][i] = ub;
+          lb4[it][i] = lbv;
           const unsigned long long m = __ballot(need);
           if (m != 0ull) {
             int qb = 0;
@@ -288,15 +299,15 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
             if (need) s_q[qb + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(off0 + i);
           }
         }
-        if (skip[0] && skip[1] && skip[2] && skip[3] && off0 + 3 < clen && (r0 & 3) == 0) {
-          *reinterpret_cast<f4v*>(ubuf + r0) = ub4;
-          *reinterpret_cast<f4v*>(lbuf + r0) = lb4;
+        if (skip[0] && skip[1] && skip[2] && skip[3]) {
+          *reinterpret_cast<f4v*>(ubuf + r0) = ub4[it];
+          *reinterpret_cast<f4v*>(lbuf + r0) = lb4[it];
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (skip[i]) {
-              ubuf[r0 + i] = ub4[i];
-              lbuf[r0 + i] = lb4[i];
+              ubuf[r0 + i] = ub4[it][i];
+              lbuf[r0 + i] = lb4[it][i];
             }
         }
       }
@@ -353,21 +364,22 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(lbuf ? (void*)(lbuf + lo) : (void*)X, lbuf ? nb * 4 : 0);
     const int tile_bytes = 64 * F * 4;
     const int kk = lane >> 4, mm = lane & 15;  // MFMA operand lane map
-    constexpr int MBX = 4;                     // label blocks of 16 kept in fp64 accumulators
-    const int MB = (k + 15) >> 4;
-    const bool mfma_m = MODE == 0 && KIND == kFirst && MB * NB <= MBX;
+    // kFirst: MBT blocks of 16 labels x NB blocks of 16 features in fp64
+    // accumulators (the launcher picks MBT = ceil(k / 16), MBT * NB <= 4)
+    constexpr int MBX = MBT * NB;
+    constexpr int MB = MBT;
+    constexpr bool mfma_m = MODE == 0 && KIND == kFirst;
     static_assert(KIND != kFirstAtomic || MODE == 0, "atomic first pass is mode 0");
     typedef double d4v __attribute__((ext_vector_type(4)));
-    d4v acc[KIND == kFirst && MODE == 0 ? MBX : 1];
+    d4v acc[mfma_m ? MBX : 1];
 #pragma unroll
-    for (int i = 0; i < (KIND == kFirst && MODE == 0 ? MBX : 1); ++i) acc[i] = d4v{0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < (mfma_m ? MBX : 1); ++i) acc[i] = d4v{0.0, 0.0, 0.0, 0.0};
     int since_flush = 0;
     auto flush = [&]() {
       if constexpr (MODE == 0 && KIND == kFirst) {
-        if (!mfma_m) return;
 #pragma unroll
         for (int i = 0; i < MBX; ++i) {
-          if (i < MB * NB) {
+          {
             const int mb = i / NB, nbk = i - mb * NB;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -455,10 +467,6 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
           continue;
         }
         if constexpr (MODE == 0 && KIND == kFirst) {
-          if (!mfma_m) {
-            move_rows(__ballot(ch), lab, 255);
-            continue;
-          }
           if (valid) atomicAdd(&s_cnt[lab], 1);
           s_lab[lane] = valid ? lab : -1;
           __builtin_amdgcn_wave_barrier();
@@ -474,11 +482,9 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
             }
 #pragma unroll
             for (int i = 0; i < MBX; ++i) {
-              if (i < MB * NB) {
-                const int mb = i / NB, nbk = i - mb * NB;
-                const double a = lr == 16 * mb + mm ? 1.0 : 0.0;
-                acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq[nbk], acc[i], 0, 0, 0);
-              }
+              const int mb = i / NB, nbk = i - mb * NB;
+              const double a = lr == 16 * mb + mm ? 1.0 : 0.0;
+              acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq[nbk], acc[i], 0, 0, 0);
             }
           }
           if (++since_flush == 32) {  // sums stay below 32 * 64 * 2^41 = 2^52: exact
@@ -598,17 +604,25 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
   const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
   const dim3 grid((unsigned)G * (unsigned)n);
-#define MW_LP(FMV, MO, KI)                                                                          \
-  hipLaunchKernelGGL((lloyd_pass_kernel<FMV, MO, KI>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, \
+  // kFirst: fp64 accumulators for ceil(kmax / 16) label blocks x the feature
+  // blocks, at most 4 (else the sums go through LDS atomics)
+  const int NBF = FM <= 16 ? 1 : FM / 16, MBF = (kmax + 15) / 16;
+  if (mode == 0 && kind == kFirst && MBF * NBF > 4) kind = kFirstAtomic;
+#define MW_LP(FMV, MO, KI, MBV)                                                                        \
+  hipLaunchKernelGGL((lloyd_pass_kernel<FMV, MO, KI, MBV>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, \
                      d_qexp, fits, n, R)
-#define MW_LPF(FMV)                                 \
-  if (mode == 0) {                                  \
-    if (kind == kFirst) MW_LP(FMV, 0, kFirst);      \
-    else if (kind == kTile) MW_LP(FMV, 0, kTile);   \
-    else if (kind == kFirstAtomic) MW_LP(FMV, 0, kFirstAtomic); \
-    else MW_LP(FMV, 0, kQueue);                     \
-  } else if (mode == 1) MW_LP(FMV, 1, kFirst);      \
-  else MW_LP(FMV, 2, kFirst);
+#define MW_LPF(FMV)                                                              \
+  if (mode == 0) {                                                               \
+    if (kind == kFirst) {                                                        \
+      if (MBF == 1) MW_LP(FMV, 0, kFirst, 1);                                    \
+      else if (MBF == 2) { if constexpr ((FMV <= 32)) MW_LP(FMV, 0, kFirst, 2); } \
+      else { if constexpr ((FMV <= 16)) MW_LP(FMV, 0, kFirst, 4); }              \
+    }                                                                            \
+    else if (kind == kTile) MW_LP(FMV, 0, kTile, 1);                            \
+    else if (kind == kFirstAtomic) MW_LP(FMV, 0, kFirstAtomic, 1);              \
+    else MW_LP(FMV, 0, kQueue, 1);                                              \
+  } else if (mode == 1) MW_LP(FMV, 1, kFirst, 1);                               \
+  else MW_LP(FMV, 2, kFirst, 1);
   if (FM == 8) { MW_LPF(8) }
   else if (FM == 16) { MW_LPF(16) }
   else if (FM == 32) { MW_LPF(32) }

@@ -275,6 +275,8 @@ class _FitState:
         self.recomputed = 0
         self.history = []  # (changed, recomputed) per pass
         self.iexp = 0
+        self.drift_max = 0.0
+        self.prev_dmax = 0.0
 
     def add(self, rec, F, qscale, a64, b64):
         """Apply a pass's record (mode 0): exact sums, sizes; returns the
@@ -298,8 +300,10 @@ class _FitState:
 
 KIND_FIRST, KIND_TILE, KIND_QUEUE = 0, 1, 2
 # a mode-0 pass streams every row (kTile) while the previous pass recomputed
-# more than this fraction of the rows, else only the undecided ones (kQueue)
-QUEUE_BELOW = float(os.environ.get("MW_LLOYD_QUEUE_BELOW", "0.25"))
+# more than this fraction of the rows, else only the undecided ones (kQueue):
+# the k = 2..20 sweep at 10k^2 x 30 (tools/sweep_bench.py) took 1.05 / 1.03 /
+# 0.90 s at 0.03 / 0.06 / 0.12
+QUEUE_BELOW = float(os.environ.get("MW_LLOYD_QUEUE_BELOW", "0.12"))
 
 
 def _launch_pass(rows, fits_g, mode, kind, par, poff, outs, st, label="lloyd_pass"):
@@ -374,6 +378,7 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
             k = fs.k
             c32 = fs.centers.astype(np.float32)
             drift, dmax, half = _bound_tables(c32, fs.prev32)
+            fs.prev_dmax = fs.drift_max if fs.prev32 is not None else 0.0
             fs.prev32, fs.drift_max = c32, dmax
             o = int(poff[g])
             host_par[o:o + k * F] = c32.ravel()
@@ -395,10 +400,17 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
     first = 3 if os.environ.get("MW_LLOYD_FIRST_ATOMIC") == "1" else KIND_FIRST
 
     def kind_of(g):
-        h = fits[g].history
-        if not h:
+        """First pass, then kTile or kQueue by the predicted share of
+        undecided rows: the last pass's share scaled by how far the centers
+        moved now relative to then (rows fail the bound test about in
+        proportion to the drift)."""
+        fs = fits[g]
+        if not fs.history:
             return first
-        return KIND_TILE if h[-1][1] > QUEUE_BELOW * S_glob else KIND_QUEUE
+        frac = fs.history[-1][1] / max(S_glob, 1)
+        if fs.prev_dmax > 0 and np.isfinite(fs.drift_max):
+            frac *= min(1.0, fs.drift_max / fs.prev_dmax)
+        return KIND_TILE if frac > QUEUE_BELOW else KIND_QUEUE
 
     S_glob = S
     if comm.sharded():

@@ -446,6 +446,69 @@ def mse_mxif(imgs, tissue_ids, features, centers, mean, scale, k):
     return out
 
 
+def percentage_variance_st(X, centers, labels):
+    """``estimate_percentage_variance_st`` (MILWRM.py:518-554): labels are the
+    section's tissue_IDs (every spot has one)."""
+    X = np.asarray(X, dtype=np.float64)
+    dc = np.concatenate([(X[labels == i] - centers[i]) ** 2 for i in pd_unique(labels)])
+    dm = (X - X.mean(axis=0)) ** 2
+    return np.sum(dc) / np.sum(dm) * 100
+
+
+def pd_unique(a):
+    """Unique values in order of appearance (pandas.unique)."""
+    _, first = np.unique(a, return_index=True)
+    return np.asarray(a)[np.sort(first)]
+
+
+def mse_st(X, label_list, n_obs, centers, k):
+    """``estimate_mse_st`` (MILWRM.py:601-644), including its slice offsets:
+    section m >= 1 reads rows from n_obs[m-1] (``i_slice = adata.n_obs``)."""
+    X = np.asarray(X, dtype=np.float64)
+    out = {}
+    for i in range(k):
+        i0, j0, diff = 0, 0, []
+        for lab, n in zip(label_list, n_obs):
+            j0 += n
+            data = X[i0:j0]
+            x = (data[np.where(lab == i)[0]] - centers[i]) ** 2
+            diff.append(np.zeros(centers.shape[1]) if len(x) == 0 else x.mean(axis=0))
+            i0 = n
+        out[i] = diff
+    return out
+
+
+def tissue_id_proportions(tissue_ids, k):
+    """``plot_tissue_ID_proportions_mxif``'s table (MILWRM.py:2040-2063):
+    domains x images, each column the domains' share of the image's labelled
+    pixels."""
+    counts = np.array([[np.sum(np.asarray(t) == j) for t in tissue_ids] for j in range(k)],
+                      dtype=np.float64)
+    return counts / counts.sum(axis=0)
+
+
+def create_tissue_mask(img_hwc, features=None, fract=0.2):
+    """``img.create_tissue_mask`` (MxIF.py:543-589): lognorm with the
+    whole-image channel means, Gaussian sigma 2, subsample, KMeans(2, 18) on
+    unscaled rows, predict all pixels, background flip."""
+    x = np.asarray(img_hwc, dtype=np.float64)
+    h, w, d = x.shape
+    x = log_normalize(x, None)
+    x = gaussian_blur(x, 2.0)
+    mask = np.ones((h, w))
+    feats = list(range(d)) if features is None else list(features)
+    X, _ = subsample_pixels(x, mask, feats, fract, 16)
+    km = kmeans_fit(X, 2, random_state=18)
+    c = km["cluster_centers_"]
+    lab = predict(x.reshape(h * w, d), c).astype(float).reshape(h, w)
+    z = (c - c.mean()) / c.std()
+    if z[0].mean() > 0:
+        lab = np.where(lab == 0.0, 0.5, lab)
+        lab = np.where(lab == 1.0, 0.0, lab)
+        lab = np.where(lab == 0.5, 1.0, lab)
+    return lab
+
+
 def confidence_st(X, centers, labels):
     """``estimate_confidence_score_st`` (MILWRM.py:557-598)."""
     X = np.asarray(X, dtype=np.float64)

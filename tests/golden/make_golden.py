@@ -11,7 +11,7 @@ sklearn 1.7.2 / SciPy 1.15.3 / NumPy 2.2.6 numerics.
 Outputs small compressed ``.npz`` fixtures next to this script.  Nothing from
 the reference is copied: the fixtures are inputs and outputs only.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [mxif_small mxif_hard256 preproc_edges st_hex qc]
 """
 from __future__ import annotations
 
@@ -296,9 +296,96 @@ def make_st_hex(MW):
     print("st_hex: k", lab.k, "n_iter", lab.kmeans.n_iter_)
 
 
+def make_qc(MW, MxIF):
+    """Clustering QC and tissue masks through the reference's own functions:
+    estimate_percentage_variance_mxif / estimate_mse_mxif (MILWRM.py:280-333,
+    453-515) on a k=4 and a k=24 labelling of the mxif_small slides,
+    tissue-ID proportions (plot_tissue_ID_proportions_mxif, MILWRM.py:2013-2073,
+    drawn to an Agg canvas), img.create_tissue_mask (MxIF.py:543-589), and the
+    ST estimators estimate_percentage_variance_st / estimate_mse_st
+    (MILWRM.py:518-554, 601-644) on the st_hex sections."""
+    import pandas as pd
+
+    shapes = (96, 128, 8)
+    raw, masks = [], []
+    for s in range(3):
+        im, m = _synth(*shapes, seed=20251015 + s, mode="hard")
+        raw.append(im)
+        masks.append(m)
+    out = {"raw": np.stack(raw), "masks": np.stack(masks)}
+    for k in (4, 24):
+        imgs = [MxIF.img(r.copy(), mask=m.copy()) for r, m in zip(raw, masks)]
+        ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
+        df = pd.DataFrame({"Img": imgs, "batch_names": ["b1", "b1", "b2"],
+                           "mean estimators": list(ests), "pixels": list(pix)})
+        lab = MW.mxif_labeler(df)
+        lab.prep_cluster_data(features=list(range(8)), filter_name="gaussian", sigma=2, fract=0.2)
+        lab.label_tissue_regions(k=k, plot_out=False, random_state=18, n_jobs=1)
+        cents = lab.kmeans.cluster_centers_
+        pv = [MW.estimate_percentage_variance_mxif(lab.image_df["Img"][i], False, lab.scaler, cents,
+                                                   list(range(8)), lab.tissue_IDs[i])
+              for i in range(3)]
+        mse = MW.estimate_mse_mxif(list(lab.image_df["Img"]), False, lab.tissue_IDs, lab.scaler,
+                                   cents, list(range(8)), k)
+        lab.plot_tissue_ID_proportions_mxif()
+        out[f"k{k}_centers"] = cents
+        out[f"k{k}_scaler_mean"] = lab.scaler.mean_
+        out[f"k{k}_scaler_scale"] = lab.scaler.scale_
+        out[f"k{k}_tissue_IDs"] = np.stack([_nan_to_i8(t) for t in lab.tissue_IDs])
+        out[f"k{k}_pct_variance"] = np.array(pv)
+        out[f"k{k}_mse"] = np.array([[mse[i][j] for j in range(3)] for i in range(k)])  # k x images x F
+        out[f"k{k}_proportions"] = lab.tissue_ID_proportion.values.astype(np.float64)
+    # create_tissue_mask on the raw slides (features=None: all channels)
+    tm = []
+    for r in raw[:2]:
+        im = MxIF.img(r.copy())
+        im.create_tissue_mask()
+        tm.append(np.asarray(im.mask, dtype=np.float64))
+    out["tissue_mask"] = np.stack(tm)
+    # ST estimators on the st_hex sections (3 copies: estimate_mse_st's slice offsets)
+    rng = np.random.default_rng(11)
+    adatas = []
+    for s, (rows, cols) in enumerate([(50, 55), (48, 52), (20, 30)]):
+        A, coords = _hex_grid(rows, cols)
+        dom = ((coords[:, 0] // 12) * 3 + coords[:, 1] // 14) % 6
+        prof = rng.normal(0, 3, size=(6, 10))
+        pcs = prof[dom] + rng.normal(0, 1.0, size=(coords.shape[0], 10))
+        adatas.append(_DuckAnnData(pcs, A))
+        out[f"st_pcs{s}"] = pcs
+        out[f"st_adj{s}_indptr"] = A.indptr
+        out[f"st_adj{s}_indices"] = A.indices
+    st = MW.st_labeler(adatas)
+    st.prep_cluster_data(use_rep="X_pca", features=None, n_rings=1,
+                         spatial_graph_key="spatial_connectivities", n_jobs=1)
+    st.label_tissue_regions(k=5, alpha=0.05, plot_out=False, random_state=18, n_jobs=1)
+    cd, cents = st.cluster_data, st.kmeans.cluster_centers_
+    pv, i0 = [], 0
+    for a in adatas:
+        pv.append(MW.estimate_percentage_variance_st(cd[i0:i0 + a.n_obs], a, cents))
+        i0 += a.n_obs
+    mse = MW.estimate_mse_st(cd, adatas, cents, 5)
+    out["st_cluster_data"] = cd
+    out["st_centers"] = cents
+    out["st_labels"] = st.kmeans.labels_
+    out["st_pct_variance"] = np.array(pv)
+    out["st_mse"] = np.array([[mse[i][j] for j in range(3)] for i in range(5)])
+    out["st_proportions"] = np.stack(
+        [a.obs["tissue_ID"].value_counts(normalize=True, sort=False).reindex(range(5)).values
+         for a in adatas]).astype(np.float64)
+    np.savez_compressed(os.path.join(HERE, "qc_small.npz"), **out)
+    print("qc_small: pct_variance k4", out["k4_pct_variance"], "k24", out["k24_pct_variance"])
+
+
 if __name__ == "__main__":
     MW, MxIF = _import_reference()
-    make_mxif_small(MW, MxIF)
-    make_mxif_hard256(MW, MxIF)
-    make_preproc_edges(MW, MxIF)
-    make_st_hex(MW)
+    which = set(sys.argv[1:]) or {"mxif_small", "mxif_hard256", "preproc_edges", "st_hex", "qc"}
+    if "mxif_small" in which:
+        make_mxif_small(MW, MxIF)
+    if "mxif_hard256" in which:
+        make_mxif_hard256(MW, MxIF)
+    if "preproc_edges" in which:
+        make_preproc_edges(MW, MxIF)
+    if "st_hex" in which:
+        make_st_hex(MW)
+    if "qc" in which:
+        make_qc(MW, MxIF)

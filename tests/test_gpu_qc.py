@@ -1,0 +1,251 @@
+"""GPU parity of the clustering QC estimators, tissue-domain proportions,
+tissue masks, the ST feature blur and the use_paths npz round trip, against
+values the reference's own functions produced (tests/golden/qc_small.npz,
+make_golden.py make_qc) and the oracle.
+
+Tolerances: the device slides and rows are fp32 (the reference float64) with
+fp64 accumulation: sums of squares within 1e-5 relative."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import milwrm_oracle as O
+
+pytestmark = pytest.mark.gpu
+FEATS = list(range(8))
+
+
+def _preprocessed_imgs(g):
+    """Our img objects for the qc_small slides, log-normalised with the batch
+    means and blurred, as prep_cluster_data leaves them."""
+    import milwrm_amd as M
+
+    imgs = [M.img(r.copy(), mask=m.copy()) for r, m in zip(g["raw"], g["masks"])]
+    ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
+    means = O.batch_means(ests, pix, ["b1", "b1", "b2"])
+    for im, b in zip(imgs, ["b1", "b1", "b2"]):
+        im.log_normalize(mean=means[b])
+        im.blurring("gaussian", sigma=2)
+    return imgs
+
+
+def _scaler(mean, scale):
+    from milwrm_amd.kmeans import StandardScaler
+
+    s = StandardScaler()
+    s.mean_, s.scale_ = np.asarray(mean, dtype=np.float64), np.asarray(scale, dtype=np.float64)
+    return s
+
+
+@pytest.mark.parametrize("k", [4, 24])
+def test_qc_mxif_vs_reference(gpu, golden, k, monkeypatch):
+    """estimate_percentage_variance_mxif / estimate_mse_mxif (MILWRM.py:280-333,
+    453-515) on the reference's own labelling; k = 24 takes two 20-domain
+    passes.  Both blur modes (materialised, and deferred: the QC pass blurs
+    into a temporary and leaves the img's raw slide in place)."""
+    from milwrm_amd import MILWRM as MW
+
+    g = golden("qc_small")
+    cents = g[f"k{k}_centers"]
+    sc = _scaler(g[f"k{k}_scaler_mean"], g[f"k{k}_scaler_scale"])
+    tids = [np.where(t < 0, np.nan, t.astype(np.float64)) for t in g[f"k{k}_tissue_IDs"]]
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MW_FUSED_BLUR", mode)
+        imgs = _preprocessed_imgs(g)
+        pv = [MW.estimate_percentage_variance_mxif(im, False, sc, cents, FEATS, t)
+              for im, t in zip(imgs, tids)]
+        np.testing.assert_allclose(pv, g[f"k{k}_pct_variance"], rtol=1e-5)
+        mse = MW.estimate_mse_mxif(imgs, False, tids, sc, cents, FEATS, k)
+        np.testing.assert_allclose(np.array([mse[i] for i in range(k)]), g[f"k{k}_mse"], rtol=2e-5,
+                                   atol=1e-9)
+        if mode == "1":
+            assert all(im._pending_blur is not None for im in imgs)  # nothing materialised
+
+
+def test_qc_int8_device_labels_and_single_feature(gpu, golden):
+    """The labeler's own int8 device label maps as tissue_ID, and a single
+    feature (the largest per-lane LDS footprint) against the oracle."""
+    import torch
+
+    from milwrm_amd import MILWRM as MW
+
+    g = golden("qc_small")
+    imgs = _preprocessed_imgs(g)
+    cents = g["k4_centers"]
+    sc = _scaler(g["k4_scaler_mean"], g["k4_scaler_scale"])
+    t8 = torch.from_numpy(g["k4_tissue_IDs"][0].copy()).cuda()
+    pv = MW.estimate_percentage_variance_mxif(imgs[0], False, sc, cents, FEATS, t8)
+    np.testing.assert_allclose(pv, g["k4_pct_variance"][0], rtol=1e-5)
+    host = imgs[0].img
+    tid = np.where(g["k4_tissue_IDs"][0] < 0, np.nan, g["k4_tissue_IDs"][0].astype(float))
+    sc1 = _scaler(g["k4_scaler_mean"][[3]], g["k4_scaler_scale"][[3]])
+    c1 = cents[:, [3]]
+    got = MW.estimate_percentage_variance_mxif(imgs[0], False, sc1, c1, [3], tid)
+    ref = O.percentage_variance_mxif(host, [3], c1, sc1.mean_, sc1.scale_, tid)
+    np.testing.assert_allclose(got, ref, rtol=1e-5)
+
+
+def test_qc_constant_feature_and_zero_denominator(gpu):
+    """A near-constant feature keeps its digits (shifted sums), and a constant
+    slide gives the reference's numpy nan (0/0) rather than an exception."""
+    import milwrm_amd as M
+    from milwrm_amd import MILWRM as MW
+
+    rng = np.random.default_rng(5)
+    a = np.empty((64, 80, 2))
+    a[:, :, 0] = 1000.0 + rng.normal(0, 1e-3, size=(64, 80))
+    a[:, :, 1] = rng.uniform(0, 5, size=(64, 80))
+    im = M.img(a.astype(np.float32).astype(np.float64), mask=np.ones((64, 80)))
+    tid = (a[:, :, 1] > 2.5).astype(float)
+    cents = np.array([[1000.0, 1.25], [1000.0, 3.75]])
+    sc = _scaler([0.0, 0.0], [1.0, 1.0])
+    got = MW.estimate_percentage_variance_mxif(im, False, sc, cents, [0, 1], tid)
+    ref = O.percentage_variance_mxif(im.img, [0, 1], cents, sc.mean_, sc.scale_, tid)
+    np.testing.assert_allclose(got, ref, rtol=1e-5)
+    flat = M.img(np.full((8, 8, 2), 3.0), mask=np.ones((8, 8)))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        v = MW.estimate_percentage_variance_mxif(flat, False, sc, np.array([[3.0, 3.0]]), [0, 1],
+                                                 np.zeros((8, 8)))
+    assert np.isnan(v)
+
+
+def test_tissue_id_proportions_mxif(gpu, golden):
+    """plot_tissue_ID_proportions_mxif (MILWRM.py:2013-2073): the per-image
+    domain shares from the label pass's counts; the plot is drawn (Agg)."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import milwrm_amd as M
+
+    g = golden("qc_small")
+    imgs = [M.img(r.copy(), mask=m.copy()) for r, m in zip(g["raw"], g["masks"])]
+    ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
+    df = pd.DataFrame({"Img": imgs, "batch_names": ["b1", "b1", "b2"],
+                       "mean estimators": list(ests), "pixels": list(pix)})
+    lab = M.mxif_labeler(df)
+    lab.prep_cluster_data(features=FEATS, sigma=2, fract=0.2)
+    lab.label_tissue_regions(k=4, plot_out=False, random_state=18)
+    ax = lab.plot_tissue_ID_proportions_mxif()
+    assert ax is not None
+    own = O.tissue_id_proportions([np.nan_to_num(t, nan=-1) for t in lab.tissue_IDs], 4)
+    np.testing.assert_allclose(lab.tissue_ID_proportion.values, own, rtol=1e-12)
+    np.testing.assert_allclose(lab.tissue_ID_proportion.values, g["k4_proportions"], atol=1e-3)
+
+
+def test_create_tissue_mask_vs_reference(gpu, golden):
+    """img.create_tissue_mask (MxIF.py:543-589) against the reference's masks
+    (labels equal except at near-ties of the 2-means), and the reference's
+    feature-count error for a feature subset."""
+    import milwrm_amd as M
+
+    g = golden("qc_small")
+    for r, ref in zip(g["raw"][:2], g["tissue_mask"]):
+        im = M.img(r.copy())
+        im.create_tissue_mask()
+        got = np.asarray(im.mask, dtype=np.float64)
+        assert got.shape == ref.shape
+        assert np.mean(got != ref) < 1e-3, np.mean(got != ref)
+    im = M.img(g["raw"][0].copy())
+    with pytest.raises(ValueError, match="features"):
+        im.create_tissue_mask(features=[0, 1, 2])
+
+
+class _Duck:
+    def __init__(self, n, labels=None, categories=None):
+        self.n_obs = n
+        self.obs = pd.DataFrame(index=[str(i) for i in range(n)])
+        if labels is not None:  # as st_labeler.label_tissue_regions sets it (MILWRM.py:1080-1089)
+            self.obs["tissue_ID"] = pd.Categorical(labels, categories=categories)
+
+
+def test_qc_st_vs_reference(gpu, golden):
+    """estimate_percentage_variance_st / estimate_mse_st (MILWRM.py:518-554,
+    601-644, including the reference's section offsets) and the ST domain
+    proportions (plot_tissue_ID_proportions_st, MILWRM.py:1400-1452)."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    from milwrm_amd import MILWRM as MW
+
+    g = golden("qc_small")
+    X, cents, labels = g["st_cluster_data"], g["st_centers"], g["st_labels"]
+    n_obs = [g[f"st_pcs{s}"].shape[0] for s in range(3)]
+    offs = np.concatenate([[0], np.cumsum(n_obs)])
+    ads = [_Duck(n_obs[s], labels[offs[s]:offs[s + 1]], np.unique(labels)) for s in range(3)]
+    pv = [MW.estimate_percentage_variance_st(X[offs[s]:offs[s + 1]], ads[s], cents) for s in range(3)]
+    np.testing.assert_allclose(pv, g["st_pct_variance"], rtol=1e-5)
+    mse = MW.estimate_mse_st(X, ads, cents, 5)
+    np.testing.assert_allclose(np.array([mse[i] for i in range(5)]), g["st_mse"], rtol=2e-5, atol=1e-9)
+    st = MW.st_labeler.__new__(MW.st_labeler)
+    st.adatas = ads
+    st.plot_tissue_ID_proportions_st()
+    np.testing.assert_allclose(st.tissue_ID_proportion.values, g["st_proportions"], rtol=1e-12)
+
+
+def test_blur_features_st_device_vs_oracle(gpu, golden):
+    """blur_features_st (ST.py:25-77) on the device CSR neighbour mean: the
+    oracle's neighbour mean on the golden hex graph, a self-loop counted twice,
+    and NaN features skipped as pandas' mean does."""
+    import scipy.sparse as sp
+
+    import milwrm_amd as M
+
+    g = golden("st_hex")
+    n = g["pcs0"].shape[0]
+    A = sp.csr_matrix((np.ones(len(g["adj0_indices"])), g["adj0_indices"], g["adj0_indptr"]),
+                      shape=(n, n)).tolil()
+    A[5, 5] = 1.0  # self-loop
+    A = A.tocsr()
+    X = g["pcs0"].copy()
+    X[7, 2] = np.nan
+    ad = _Duck(n)
+    ad.obsp = {"g": A}
+    tmp = pd.DataFrame(X, columns=[f"X_pca_{i}" for i in range(X.shape[1])])
+    got = M.blur_features_st(ad, tmp, spatial_graph_key="g").values
+    ref = np.empty_like(X)
+    for x in range(n):
+        nb = list(A.indices[A.indptr[x]:A.indptr[x + 1]]) + [x]
+        ref[x] = pd.DataFrame(X[nb]).mean().values
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(ad.obs["blur_X_pca_0"].values, ref[:, 0], rtol=1e-12)
+
+
+def test_use_paths_npz_round_trip(gpu, golden, tmp_path):
+    """mxif_labeler with image paths (MILWRM.py:205-233, 258-260): npz in,
+    preprocessed npz out under _final_preprocessed_images, labels and
+    confidences equal to the in-memory run."""
+    import milwrm_amd as M
+
+    g = golden("mxif_small")
+    paths = []
+    for i in range(3):
+        p = str(tmp_path / f"slide{i}")
+        M.img(g["raw"][i].copy(), mask=g["masks"][i].copy()).to_npz(p)
+        paths.append(p)
+    ests, pix = zip(*[M.img.from_npz(p + ".npz").calculate_non_zero_mean() for p in paths])
+    df = pd.DataFrame({"Img": paths, "batch_names": ["b1", "b1", "b2"],
+                       "mean estimators": list(ests), "pixels": list(pix)})
+    lab = M.mxif_labeler(df)
+    assert lab.use_paths
+    with pytest.raises(Exception, match="requird"):
+        lab.prep_cluster_data(features=FEATS, sigma=2, fract=0.2)
+    lab.prep_cluster_data(features=FEATS, sigma=2, fract=0.2, path_save=str(tmp_path))
+    saved = list(lab.image_df["Img"])
+    assert all(p.endswith("_final_preprocessed") for p in saved)
+    assert all((tmp_path / "_final_preprocessed_images" / (p.split("/")[-1] + ".npz")).exists()
+               for p in saved)
+    lab.label_tissue_regions(k=4, plot_out=False, random_state=18)
+    lab.confidence_score_images()
+    imgs = [M.img(g["raw"][i].copy(), mask=g["masks"][i].copy()) for i in range(3)]
+    ests2, pix2 = zip(*[im.calculate_non_zero_mean() for im in imgs])
+    df2 = pd.DataFrame({"Img": imgs, "batch_names": ["b1", "b1", "b2"],
+                        "mean estimators": list(ests2), "pixels": list(pix2)})
+    mem = M.mxif_labeler(df2)
+    mem.prep_cluster_data(features=FEATS, sigma=2, fract=0.2)
+    mem.label_tissue_regions(k=4, plot_out=False, random_state=18)
+    mem.confidence_score_images()
+    np.testing.assert_array_equal(lab.kmeans.cluster_centers_, mem.kmeans.cluster_centers_)
+    for i in range(3):
+        np.testing.assert_array_equal(np.nan_to_num(lab.tissue_IDs[i], nan=-1),
+                                      np.nan_to_num(mem.tissue_IDs[i], nan=-1))
+    np.testing.assert_array_equal(lab.confidence_score_df.values, mem.confidence_score_df.values)

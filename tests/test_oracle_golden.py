@@ -152,3 +152,53 @@ def test_st_plumbing(golden):
     n0 = g["pcs0"].shape[0]
     c0, _ = O.confidence_st(Xs[:n0], r["cluster_centers_"], r["labels_"][:n0])
     np.testing.assert_allclose(c0, g["conf0"], rtol=1e-9)
+
+
+# ---- QC estimators, proportions, tissue masks (tests/golden/qc_small.npz) ----
+
+def _qc_images(g):
+    """The mxif_small slides preprocessed as the reference does before QC
+    (batch means, log-normalise, Gaussian) -> host float64 HWC."""
+    raw, masks = g["raw"], g["masks"]
+    ests, pix = zip(*[O.non_zero_mean(r) for r in raw])
+    means = O.batch_means(ests, pix, ["b1", "b1", "b2"])
+    out = []
+    for r, b in zip(raw, ["b1", "b1", "b2"]):
+        out.append(O.gaussian_blur(O.log_normalize(r, means[b]), 2.0))
+    return out
+
+
+@pytest.mark.parametrize("k", [4, 24])
+def test_qc_mxif_oracle(golden, k):
+    g = golden("qc_small")
+    imgs = _qc_images(g)
+    cents, mean, scale = g[f"k{k}_centers"], g[f"k{k}_scaler_mean"], g[f"k{k}_scaler_scale"]
+    tids = [np.where(t < 0, np.nan, t.astype(np.float64)) for t in g[f"k{k}_tissue_IDs"]]
+    pv = [O.percentage_variance_mxif(im, list(range(8)), cents, mean, scale, t)
+          for im, t in zip(imgs, tids)]
+    np.testing.assert_allclose(pv, g[f"k{k}_pct_variance"], rtol=1e-10)
+    mse = O.mse_mxif(imgs, tids, list(range(8)), cents, mean, scale, k)
+    np.testing.assert_allclose(np.array([mse[i] for i in range(k)]), g[f"k{k}_mse"], rtol=1e-10,
+                               atol=1e-14)
+    np.testing.assert_allclose(O.tissue_id_proportions(g[f"k{k}_tissue_IDs"], k),
+                               g[f"k{k}_proportions"], rtol=1e-12)
+
+
+def test_qc_st_oracle(golden):
+    g = golden("qc_small")
+    X, cents, labels = g["st_cluster_data"], g["st_centers"], g["st_labels"]
+    n_obs = [g[f"st_pcs{s}"].shape[0] for s in range(3)]
+    offs = np.concatenate([[0], np.cumsum(n_obs)])
+    labs = [labels[offs[s]:offs[s + 1]] for s in range(3)]
+    pv = [O.percentage_variance_st(X[offs[s]:offs[s + 1]], cents, labs[s]) for s in range(3)]
+    np.testing.assert_allclose(pv, g["st_pct_variance"], rtol=1e-10)
+    mse = O.mse_st(X, labs, n_obs, cents, 5)
+    np.testing.assert_allclose(np.array([mse[i] for i in range(5)]), g["st_mse"], rtol=1e-10)
+    props = np.stack([np.bincount(l, minlength=5) / len(l) for l in labs])
+    np.testing.assert_allclose(props, g["st_proportions"], rtol=1e-12)
+
+
+def test_create_tissue_mask_oracle(golden):
+    g = golden("qc_small")
+    for r, ref in zip(g["raw"][:2], g["tissue_mask"]):
+        np.testing.assert_array_equal(O.create_tissue_mask(r), ref)
