@@ -33,6 +33,17 @@ METRIC = "pixels/sec (node) for preprocess+k-means fit+label, 30-ch MxIF k=8; %H
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); measured copy ceiling ~6300
 
 
+def _config_name(H, W, C):
+    """Which BASELINE.json config one GPU's slice of this workload is."""
+    if (H, W, C) == (10000, 10000, 30):
+        return "BASELINE config 2 per GPU"
+    if (H, W, C) == (20000, 20000, 30):
+        return "BASELINE config 3 per GPU: one of its 8 slides"
+    if (H, W, C) == (40000, 40000, 50):
+        return "BASELINE config 5 per GPU: one of its 16 slides (one slide per GPU step)"
+    return "custom size"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,7 +158,9 @@ def main():
         cpr = cProfile.Profile()
         cpr.enable()
     t0 = time.perf_counter()
+    lab = None
     for _ in range(args.steps):
+        lab = None  # the last step's buffers go before the next step allocates (40k^2 x 50 fits once)
         lab = step()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -194,7 +207,8 @@ def main():
         "dtype": "f32 (fp64 accumulation)",
         "data": "synthetic (device-generated Voronoi/gamma slides, SURVEY 8d; uint16 HWC + mask)",
         "config": {"workload": f"mxif_labeler: {world} x synthetic {C}-ch {H}x{W} slide (one per GPU), "
-                               f"k={k}, sigma=2, fract=0.2, random_state=18 (BASELINE config 2 per GPU)",
+                               f"k={k}, sigma=2, fract=0.2, random_state=18 ({_config_name(H, W, C)})",
+                   "blur": "deferred (fused epilogues)" if D.defer_blur(H, W, C) else "materialised",
                    "slides_per_gpu": 1, "H": H, "W": W, "C": C, "k": k, "mode": args.mode,
                    "samples_per_slide": S, "lloyd_iters": n_iter, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,

@@ -22,8 +22,8 @@ import pandas as pd
 import torch
 
 from . import device as D
-from .assign import (assign_image, assign_rows, blur_assign_image, dm_total, domain_means,
-                     domain_sse_image, domain_sse_rows)
+from .assign import (assign_image, assign_rows, banded_assign_image, blur_assign_image, dm_total,
+                     domain_means, domain_sse_image, domain_sse_rows)
 from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
@@ -211,19 +211,26 @@ def estimate_mse_st(cluster_data, adatas, centroids, k):
 def _assign_img(image: img, features, centers, scaler):
     feats = image._features(features)
     mu, inv = scaler.affine()
-    if image._pending_blur is not None and feats == list(range(image.n_ch)):
-        # deferred blur (D.defer_blur): label + confidence straight from the
-        # raw slide, the blurred slide is recomputed in registers and LDS
+    centers = np.asarray(centers, dtype=np.float64)
+    if image._pending_blur is not None:
+        # deferred blur (D.defer_blur: the fp32 blurred slide does not fit
+        # HBM): blur band by band into a reused buffer and label each band
+        # (MW_DEFERRED_ASSIGN=band, the default), or recompute the blur
+        # inside the fused assign epilogue (=fused, or when no band fits)
         sigma, truncate = image._pending_blur
         inv_mean, p = image._pending
-        res = blur_assign_image(image._device(), sigma, inv_mean, p, mu, inv,
-                                np.asarray(centers, dtype=np.float64), image._mask_device(),
-                                truncate=truncate)
+        how = os.environ.get("MW_DEFERRED_ASSIGN", "band")
+        res = None
+        if how != "fused":
+            res = banded_assign_image(image._device(), sigma, inv_mean, p, feats, mu, inv, centers,
+                                      image._mask_device(), truncate=truncate)
+        if res is None and feats == list(range(image.n_ch)):
+            res = blur_assign_image(image._device(), sigma, inv_mean, p, mu, inv, centers,
+                                    image._mask_device(), truncate=truncate)
         if res is not None:
             return res
     src = D.as_float32(image._materialize())
-    return assign_image(src, feats, mu, inv, np.asarray(centers, dtype=np.float64),
-                        image._mask_device())
+    return assign_image(src, feats, mu, inv, centers, image._mask_device())
 
 
 def _gather_deferred(image: img, feat, idx, r2p, X_out) -> bool:

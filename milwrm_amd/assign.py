@@ -2,6 +2,8 @@
 ``estimate_confidence_score_mxif``, MILWRM.py:237-277 and 389-450) on device."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -11,7 +13,7 @@ from . import profiling
 
 
 def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
-                 mask_u8: torch.Tensor):
+                 mask_u8: torch.Tensor, out_lab=None, out_conf=None):
     """One streaming pass over an HWC fp32 image.
 
     Returns (labels int8 [H,W] with -1 outside the mask, conf fp32 [H,W] with
@@ -26,8 +28,9 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
               .astype(np.float32), dev)
     c32 = D.h2d(np.asarray(centers, dtype=np.float32), dev)
     n = H * W
-    lab = torch.empty((H, W), dtype=torch.int8, device=dev)
-    conf = torch.empty((H, W), dtype=torch.float32, device=dev)
+    lab = torch.empty((H, W), dtype=torch.int8, device=dev) if out_lab is None else out_lab
+    conf = torch.empty((H, W), dtype=torch.float32, device=dev) if out_conf is None else out_conf
+    assert lab.is_contiguous() and conf.is_contiguous() and lab.numel() == n and conf.numel() == n
     dom = torch.empty(2 * k, dtype=torch.float64, device=dev)
     ws = D.WS.get("assign", N.query("mw_assign_ws_bytes", n, k))
     st = D.stream()
@@ -72,6 +75,48 @@ def blur_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: floa
     with profiling.timed("domain_records", n * 5):
         N.call("mw_domain_records", D.P(lab), D.P(conf), n, C, k, D.P(ws), st)
     N.call("mw_assign_reduce", D.P(ws), n, k, D.P(dom), st)
+    return lab, conf, dom
+
+
+def banded_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
+                        inv, centers: np.ndarray, mask_u8: torch.Tensor, truncate: float = 4.0,
+                        band_rows=None):
+    """``assign_image(blur(lognorm(raw)))`` for a slide whose fp32 blurred copy
+    does not fit HBM: the blur is materialised one band of rows at a time
+    (band plus r halo rows of input; the kernel's arithmetic per output value
+    does not depend on the band, so labels and confidences are bitwise those
+    of the whole-slide blur) into one reused buffer, and each band goes
+    through the label pass.  The per-domain sums are added band after band.
+    None when not even a 16-row band fits in half the free HBM."""
+    H, W, C = raw.shape
+    k, F = centers.shape
+    w = D.gaussian_taps(sigma, truncate)
+    r = (len(w) - 1) // 2
+    row_bytes = W * C * 4
+    if band_rows is None:
+        env = os.environ.get("MW_ASSIGN_BAND_ROWS")
+        if env:
+            band_rows = int(env)
+        else:
+            free, _ = torch.cuda.mem_get_info()
+            band_rows = int(free // 2 // row_bytes) - 2 * r
+    if band_rows < 16:
+        return None
+    band_rows = min(band_rows, H)
+    dev = raw.device
+    lab = torch.empty((H, W), dtype=torch.int8, device=dev)
+    conf = torch.empty((H, W), dtype=torch.float32, device=dev)
+    dom = torch.zeros(2 * k, dtype=torch.float64, device=dev)
+    buf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=dev)
+    for y0 in range(0, H, band_rows):
+        y1 = min(H, y0 + band_rows)
+        a, b = max(0, y0 - r), min(H, y1 + r)
+        out = buf[:b - a]
+        D.blur(raw[a:b], sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
+        _, _, d = assign_image(out[y0 - a:y1 - a], feat_idx, mu, inv, centers, mask_u8[y0:y1],
+                               out_lab=lab[y0:y1], out_conf=conf[y0:y1])
+        dom += d
+    D.FUSED_USED["assign_banded"] += 1
     return lab, conf, dom
 
 

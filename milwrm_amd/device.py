@@ -296,7 +296,7 @@ def col_stats_rows(X: torch.Tensor, stats: torch.Tensor, accumulate: bool):
     N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
 
 
-FUSED_USED = {"sample": 0, "assign": 0}  # fused-epilogue launches taken (tests read it)
+FUSED_USED = {"sample": 0, "assign": 0, "assign_banded": 0}  # deferred-blur paths taken (tests read it)
 
 
 def defer_blur(H: int, W: int, C: int) -> bool:

@@ -284,19 +284,25 @@ def _mxif_labeler_from(g, n):
     return M.mxif_labeler(df)
 
 
-@pytest.fixture(params=["0", "1"], ids=["materialised", "fused"])
+@pytest.fixture(params=["0", "fused", "band"], ids=["materialised", "fused", "banded"])
 def blur_mode(request, monkeypatch):
     """Run a pipeline test with the blurred slide materialised and with the
-    blur deferred into the fused sample / assign epilogues (MW_FUSED_BLUR);
-    in fused mode the fused kernels must actually have run."""
+    blur deferred (MW_FUSED_BLUR=1): into the fused sample / assign epilogues,
+    or with the label pass over 40-row bands blurred one at a time; the
+    deferred paths must actually have run."""
     from milwrm_amd import device as D
 
-    monkeypatch.setenv("MW_FUSED_BLUR", request.param)
+    deferred = request.param != "0"
+    monkeypatch.setenv("MW_FUSED_BLUR", "1" if deferred else "0")
+    if deferred:
+        monkeypatch.setenv("MW_DEFERRED_ASSIGN", request.param)
+        monkeypatch.setenv("MW_ASSIGN_BAND_ROWS", "40")
     before = dict(D.FUSED_USED)
     yield request.param
-    if request.param == "1":
+    if deferred:
         assert D.FUSED_USED["sample"] > before["sample"], "fused sample epilogue not taken"
-        assert D.FUSED_USED["assign"] > before["assign"], "fused assign epilogue not taken"
+        key = "assign" if request.param == "fused" else "assign_banded"
+        assert D.FUSED_USED[key] > before[key], f"deferred label pass ({key}) not taken"
 
 
 def test_mxif_labeler_end_to_end_small(gpu, golden, blur_mode):
