@@ -250,6 +250,28 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
 /* per-column max |x| of S x F fp32 rows (F <= 256), fp32 out */
 int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream);
 
+/* ---- whole fit: sklearn KMeans(algorithm="lloyd").fit (_kmeans.py:1427-1554)
+ * Replaces the reference's `KMeans(n_clusters=k, random_state=seed).fit(X)`
+ * (MILWRM.py:706-737 find_tissue_regions; MILWRM.py:29-54 kMeansRes) for a
+ * caller of the C ABI.  Rows: S x F raw fp32 on the device, scaled on the fly
+ * x' = (x - mu) * inv (fp64 host arrays; pass mu = 0, inv = 1 for rows that
+ * are already standardised).  k-means++ seeded from RandomState(seed) (or the
+ * k x F scaled centers h_init, then no seeding), Lloyd with sklearn's strict
+ * and tolerance convergence (tol relative: tol * mean of the scaled rows'
+ * per-feature variance, taken from h_feature_var[F] when given, else computed
+ * on the device), empty-cluster relocation, the extra E-step and inertia.
+ * Outputs: d_labels (S uint8, device), h_centers (k x F fp64, scaled space),
+ * *h_inertia, *h_n_iter, h_init_idx (k int64, may be NULL; untouched with
+ * h_init).  Same numbers as the Python KMeans.fit on the same rows.  Caps:
+ * 1 <= k <= 64 (labels are uint8, centers live in LDS), 1 <= F <= 64 (one
+ * feature per lane of a wave); S >= k.  Allocates and frees its own device
+ * workspace; synchronises `stream` before returning. */
+int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
+                  const double* h_inv, const double* h_feature_var, int k,
+                  const double* h_init, uint32_t seed, int max_iter, double tol,
+                  uint8_t* d_labels, double* h_centers, double* h_inertia, int* h_n_iter,
+                  int64_t* h_init_idx, void* stream);
+
 /* ---- empty-cluster relocation support (_k_means_common.pyx:181-226) ---------
  * fp64 distance of every row to centers[labels]; returns the n largest
  * (value desc, index asc) into d_top_idx / d_top_val (n <= 64). */

@@ -445,7 +445,10 @@ class mxif_labeler(tissue_labeler):
         counts = [int(M * fract) for _, M in ranks]
         F = len(images[0]._features(features))
         X = torch.empty((sum(counts), F), dtype=torch.float32, device=dev)
-        stats = torch.zeros(1 + 2 * F, dtype=torch.float64, device=dev)
+        # per-image column statistics [n, mean, M2], merged on the host in
+        # image order (comm.merge_image_stats): the same merge sequence for any
+        # sharding of the images over ranks, so the scaler is bitwise the same
+        img_stats = torch.zeros((len(images), 1 + 2 * F), dtype=torch.float64, device=dev)
         # phase 2: fused lognorm+blur, gather rows into X (image_df order)
         off = 0
         paths = []
@@ -460,10 +463,10 @@ class mxif_labeler(tissue_labeler):
                 totals.append((tot, S))
                 feat = D.h2d(np.asarray(im._features(features), dtype=np.int32), dev)
                 if _gather_deferred(im, feat, idx, r2p, X[off:off + S]):
-                    D.col_stats_rows(X[off:off + S], stats, accumulate=off > 0)
+                    D.col_stats_rows(X[off:off + S], img_stats[n_img], accumulate=False)
                 else:
                     D.gather_rows(D.as_float32(im._materialize()), feat, idx, r2p, X[off:off + S],
-                                  stats, accumulate=off > 0)
+                                  img_stats[n_img], accumulate=False)
             off += S
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))
@@ -474,7 +477,7 @@ class mxif_labeler(tissue_labeler):
             self._images = images
         for tot, S in totals:
             check_total(tot, S)
-        st = comm.merge_stats(D.d2h(stats), F)
+        st = comm.merge_image_stats(D.d2h(img_stats), F)
         self.scaler = StandardScaler.from_stats(st)
         mu, inv = self.scaler.affine()
         self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv)

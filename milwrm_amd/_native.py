@@ -63,6 +63,8 @@ _PROTOS = {
     "mw_lloyd_rec_len": (c_i32, [c_i32, c_i32]),
     "mw_lloyd_pass": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "mw_col_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_kmeans_fit": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_u32, c_i32,
+                              C.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mw_farthest_ws_bytes": (c_sz, [c_i64]),
     "mw_farthest": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_ws_bytes": (c_sz, [c_i64, c_i32]),

@@ -1,0 +1,465 @@
+// mw_kmeans_fit: sklearn KMeans(algorithm="lloyd").fit as one C entry
+// (sklearn _kmeans.py:1427-1554; MILWRM calls it at MILWRM.py:706-737 and,
+// per k, in kMeansRes MILWRM.py:29-54), for callers that bind the C ABI
+// rather than the Python package.  The host control flow is the one of
+// milwrm_amd/kmeans.py (KMeans.fit -> _kmeans_plusplus_device -> lloyd_fits
+// with one fit), step for step and with the same fp64 expressions, so both
+// front ends return bitwise the same centers, labels, inertia and n_iter:
+//   * tolerance: tol * mean(var of the scaled rows)      (_kmeans.py:279-287)
+//   * k-means++ from RandomState(seed): the choice draw, then n_local_trials
+//     = 2 + int(ln k) uniforms per step                 (_kmeans.py:174-272)
+//   * Lloyd: mw_lloyd_pass per iteration (exact fixed-point sums), strict
+//     convergence on zero changed labels, else the center-shift test;
+//     empty-cluster relocation and averaging   (_k_means_common.pyx:181-311)
+//   * the extra E-step when not strictly converged, and the inertia.
+// numpy's reductions used by the Python side (pairwise sums) are restated
+// (np_sum) so the host arithmetic matches it bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace mw {
+void mt_init_genrand(uint32_t seed, uint32_t* mt);
+void mt_regen(uint32_t* mt);
+
+namespace {
+
+// numpy RandomState(seed) (MT19937, init_genrand) -> random_sample()
+struct LegacyRandom {
+  uint32_t mt[624];
+  int pos = 624;
+  explicit LegacyRandom(uint32_t seed) { mt_init_genrand(seed, mt); }
+  uint32_t next() {
+    if (pos >= 624) { mt_regen(mt); pos = 0; }
+    uint32_t y = mt[pos++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9D2C5680u;
+    y ^= (y << 15) & 0xEFC60000u;
+    y ^= y >> 18;
+    return y;
+  }
+  double sample() {  // genrand_res53
+    const uint32_t a = next() >> 5, b = next() >> 6;
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+};
+
+// numpy's pairwise_sum of a contiguous double run (n <= 128: eight partial
+// sums, combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail)
+double np_sum(const double* a, int64_t n) {
+  if (n < 8) {
+    double r = 0.0;  // numpy: -0.0 start only for n == 0 paths we never take
+    for (int64_t i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_sum(a, n2) + np_sum(a + n2, n - n2);
+}
+
+// RandomState.choice(n, p=ones(n)/n) given its uniform draw u
+// (cdf = sequential cumsum of 1/n, normalised by its last entry,
+// searchsorted 'right')
+int64_t first_center_index(int64_t n, double u) {
+  const double p = 1.0 / (double)n;
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s += p;
+  const double total = s;
+  s = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    s += p;
+    if (s / total > u) return i;
+  }
+  return n;
+}
+
+int exp_below(double bound) {  // e with bound * 2^e <= 2^40 (0 for 0)
+  if (!std::isfinite(bound) || bound <= 0.0) return 0;
+  int e;
+  std::frexp(bound, &e);
+  return 40 - e;
+}
+
+float round_f32(double x, bool up) {
+  float f = (float)x;
+  if (up && (double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+  if (!up && (double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return f;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+#define MW_TRY(call)                 \
+  do {                               \
+    const int rc_ = (call);          \
+    if (rc_ != MW_OK) return rc_;    \
+  } while (0)
+
+template <typename T>
+int dev_alloc(DevBuf& b, size_t n) {
+  MW_HIP(hipMalloc(&b.p, std::max<size_t>(n * sizeof(T), 256)));
+  return MW_OK;
+}
+
+struct Fit {
+  int64_t S;
+  int F, k;
+  hipStream_t st;
+  const float* X;
+  float *a32, *b32, *par;
+  int32_t* qexp;
+  uint8_t* labels;
+  float *ub, *lb;
+  void* ws;
+  double* out;
+  int rl;
+  std::vector<double> a64, b64;
+  std::vector<float> prev32;
+  bool have_prev = false;
+  float drift_max = 0.f, prev_dmax = 0.f;
+
+  // centers / drift / half-separation tables of the next pass (kmeans.py
+  // _bound_tables; the values only steer which rows skip the E-step)
+  int upload(const std::vector<double>& c) {
+    std::vector<float> h((size_t)k * F + 2 * k);
+    for (size_t i = 0; i < (size_t)k * F; ++i) h[i] = (float)c[i];
+    std::vector<double> drift(k, 0.0), half(k, std::numeric_limits<double>::infinity()), tmp(F);
+    for (int j = 0; j < k; ++j) {
+      if (have_prev) {
+        for (int f = 0; f < F; ++f) {
+          const double d = (double)h[(size_t)j * F + f] - (double)prev32[(size_t)j * F + f];
+          tmp[f] = d * d;
+        }
+        drift[j] = std::sqrt(np_sum(tmp.data(), F));
+      }
+      if (k > 1) {
+        double m = std::numeric_limits<double>::infinity();
+        for (int i = 0; i < k; ++i) {
+          if (i == j) continue;
+          for (int f = 0; f < F; ++f) {
+            const double d = (double)h[(size_t)j * F + f] - (double)h[(size_t)i * F + f];
+            tmp[f] = d * d;
+          }
+          m = std::min(m, np_sum(tmp.data(), F));
+        }
+        half[j] = 0.5 * std::sqrt(m);
+      }
+    }
+    float dmax = 0.f;
+    for (int j = 0; j < k; ++j) {
+      const float d32 = round_f32(drift[j], true);
+      h[(size_t)k * F + j] = d32;
+      dmax = j == 0 ? d32 : std::max(dmax, d32);
+      h[(size_t)k * F + k + j] = round_f32(half[j], false);
+    }
+    prev_dmax = have_prev ? drift_max : 0.f;
+    drift_max = dmax;
+    prev32.assign(h.begin(), h.begin() + (size_t)k * F);
+    have_prev = true;
+    MW_HIP(hipMemcpyAsync(par, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    return MW_OK;
+  }
+
+  int pass(int mode, int kind, int iexp, std::vector<double>& rec) {
+    mw_lloyd_fit f{};
+    f.centers = par;
+    f.drift = par + (size_t)k * F;
+    f.half_sep = par + (size_t)k * F + k;
+    f.labels = labels;
+    f.ub = ub;
+    f.lb = lb;
+    f.ws = ws;
+    f.out = out;
+    f.k = k;
+    f.drift_max = drift_max;
+    f.inertia_exp = iexp;
+    MW_TRY(mw_lloyd_pass(X, S, F, a32, b32, qexp, 1, &f, mode, kind, st));
+    rec.resize(rl);
+    MW_HIP(hipMemcpyAsync(rec.data(), out, rl * sizeof(double), hipMemcpyDeviceToHost, st));
+    MW_HIP(hipStreamSynchronize(st));
+    return MW_OK;
+  }
+
+  // raw rows idx[i] -> scaled fp64 (x - mu) * inv
+  int scaled_rows(const int64_t* idx, int n, const double* mu, const double* inv,
+                  std::vector<double>& outv) {
+    std::vector<float> r((size_t)F);
+    outv.resize((size_t)n * F);
+    for (int i = 0; i < n; ++i) {
+      MW_HIP(hipMemcpyAsync(r.data(), X + idx[i] * F, F * sizeof(float), hipMemcpyDeviceToHost, st));
+      MW_HIP(hipStreamSynchronize(st));
+      for (int f = 0; f < F; ++f) outv[(size_t)i * F + f] = ((double)r[f] - mu[f]) * inv[f];
+    }
+    return MW_OK;
+  }
+};
+
+}  // namespace
+}  // namespace mw
+
+using namespace mw;
+
+extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
+                             const double* h_inv, const double* h_feature_var, int k,
+                             const double* h_init, uint32_t seed, int max_iter, double tol,
+                             uint8_t* d_labels, double* h_centers, double* h_inertia, int* h_n_iter,
+                             int64_t* h_init_idx, void* stream) {
+  MW_CHECK_ARG(d_X && h_mu && h_inv && d_labels && h_centers && h_inertia && h_n_iter,
+               "mw_kmeans_fit: null pointer");
+  MW_CHECK_ARG(F >= 1 && F <= 64, "mw_kmeans_fit: F=%d outside [1, 64]", F);
+  MW_CHECK_ARG(k >= 1 && k <= 64, "mw_kmeans_fit: n_clusters=%d outside [1, 64]", k);
+  MW_CHECK_ARG(S >= k, "mw_kmeans_fit: n_samples=%lld should be >= n_clusters=%d", (long long)S, k);
+  MW_CHECK_ARG(max_iter >= 1 && tol >= 0.0, "mw_kmeans_fit: bad max_iter / tol");
+  const int T = 2 + (int)std::log((double)k);
+  MW_CHECK_ARG(h_init || T <= 8, "mw_kmeans_fit: n_local_trials > 8");
+  hipStream_t st = as_stream(stream);
+
+  Fit fit;
+  fit.S = S;
+  fit.F = F;
+  fit.k = k;
+  fit.st = st;
+  fit.X = d_X;
+  fit.rl = mw_lloyd_rec_len(k, F);
+  DevBuf b_small, b_par, b_ub, b_lb, b_ws, b_out, b_kpp, b_far, b_idx, b_cs;
+  // small: a32[F] b32[F] qexp[F] absmax[F] mu64[F] inv64[F] c64[k F] topv[64] topi[64] stats[1+2F]
+  const size_t small = 4 * 64 * 4 + 2 * 64 * 8 + 64 * 64 * 8 + 64 * 8 + 64 * 8 + 130 * 8;
+  MW_TRY(dev_alloc<char>(b_small, small));
+  char* sp = reinterpret_cast<char*>(b_small.p);
+  fit.a32 = reinterpret_cast<float*>(sp);
+  fit.b32 = fit.a32 + 64;
+  fit.qexp = reinterpret_cast<int32_t*>(fit.b32 + 64);
+  float* d_absmax = reinterpret_cast<float*>(fit.qexp + 64);
+  double* d_mu = reinterpret_cast<double*>(d_absmax + 64);
+  double* d_inv = d_mu + 64;
+  double* d_c64 = d_inv + 64;
+  double* d_topv = d_c64 + 64 * 64;
+  int64_t* d_topi = reinterpret_cast<int64_t*>(d_topv + 64);
+  double* d_stats = reinterpret_cast<double*>(d_topi + 64);
+  MW_TRY(dev_alloc<float>(b_par, (size_t)k * F + 2 * k));
+  fit.par = reinterpret_cast<float*>(b_par.p);
+  MW_TRY(dev_alloc<float>(b_ub, S));
+  MW_TRY(dev_alloc<float>(b_lb, S));
+  fit.ub = reinterpret_cast<float*>(b_ub.p);
+  fit.lb = reinterpret_cast<float*>(b_lb.p);
+  MW_TRY(dev_alloc<char>(b_ws, mw_lloyd_ws_bytes(S, k, F)));
+  fit.ws = b_ws.p;
+  MW_TRY(dev_alloc<double>(b_out, fit.rl));
+  fit.out = reinterpret_cast<double*>(b_out.p);
+  fit.labels = d_labels;
+
+  // folded scaler: x' = x * a + b (fp32), as DeviceRows
+  std::vector<float> a32(F), b32(F);
+  fit.a64.resize(F);
+  fit.b64.resize(F);
+  for (int f = 0; f < F; ++f) {
+    a32[f] = (float)h_inv[f];
+    b32[f] = (float)(-h_mu[f] * h_inv[f]);
+    fit.a64[f] = (double)a32[f];
+    fit.b64[f] = (double)b32[f];
+  }
+  MW_HIP(hipMemcpyAsync(fit.a32, a32.data(), F * 4, hipMemcpyHostToDevice, st));
+  MW_HIP(hipMemcpyAsync(fit.b32, b32.data(), F * 4, hipMemcpyHostToDevice, st));
+  MW_HIP(hipMemcpyAsync(d_mu, h_mu, F * 8, hipMemcpyHostToDevice, st));
+  MW_HIP(hipMemcpyAsync(d_inv, h_inv, F * 8, hipMemcpyHostToDevice, st));
+
+  // tolerance: tol * mean over features of the scaled rows' variance
+  double tol_abs = 0.0;
+  if (tol > 0.0) {
+    std::vector<double> var(F);
+    if (h_feature_var) {
+      for (int f = 0; f < F; ++f) var[f] = h_feature_var[f];
+    } else {
+      DevBuf b_g;
+      MW_TRY(dev_alloc<char>(b_g, mw_gather_ws_bytes(S, F)));
+      MW_TRY(mw_col_stats_rows(d_X, S, F, b_g.p, st));
+      MW_TRY(mw_col_stats_finalize(b_g.p, S, F, d_stats, 0, st));
+      std::vector<double> hs(1 + 2 * F);
+      MW_HIP(hipMemcpyAsync(hs.data(), d_stats, hs.size() * 8, hipMemcpyDeviceToHost, st));
+      MW_HIP(hipStreamSynchronize(st));
+      for (int f = 0; f < F; ++f) var[f] = hs[1 + F + f] / hs[0] * h_inv[f] * h_inv[f];
+    }
+    tol_abs = np_sum(var.data(), F) / (double)F * tol;
+  }
+
+  // fixed-point exponents of the M-step from the column max |x|
+  MW_TRY(mw_col_absmax(d_X, S, F, d_absmax, st));
+  std::vector<float> xmax(F);
+  MW_HIP(hipMemcpyAsync(xmax.data(), d_absmax, F * 4, hipMemcpyDeviceToHost, st));
+  MW_HIP(hipStreamSynchronize(st));
+  std::vector<int32_t> qe(F);
+  std::vector<double> qscale(F);
+  for (int f = 0; f < F; ++f) {
+    qe[f] = exp_below((double)xmax[f]);
+    qscale[f] = std::ldexp(1.0, -qe[f]);
+  }
+  MW_HIP(hipMemcpyAsync(fit.qexp, qe.data(), F * 4, hipMemcpyHostToDevice, st));
+
+  // initial centers
+  std::vector<double> centers((size_t)k * F);
+  if (h_init) {
+    std::memcpy(centers.data(), h_init, centers.size() * sizeof(double));
+  } else {
+    LegacyRandom rs(seed);
+    const double u0 = rs.sample();
+    const int64_t first = first_center_index(S, u0);
+    MW_TRY(dev_alloc<char>(b_kpp, mw_kpp_ws_bytes(S, T)));
+    MW_TRY(mw_kpp_init(d_X, S, F, d_mu, d_inv, d_X + first * F, T, b_kpp.p, st));
+    std::vector<double> u(T);
+    for (int c = 1; c < k; ++c) {
+      for (int t = 0; t < T; ++t) u[t] = rs.sample();
+      MW_TRY(mw_kpp_step(d_X, S, F, d_mu, d_inv, c, u.data(), T, b_kpp.p, st));
+    }
+    MW_TRY(dev_alloc<int64_t>(b_idx, k));
+    MW_TRY(mw_kpp_indices(b_kpp.p, S, T, k, reinterpret_cast<int64_t*>(b_idx.p), st));
+    std::vector<int64_t> idx(k);
+    MW_HIP(hipMemcpyAsync(idx.data(), b_idx.p, k * 8, hipMemcpyDeviceToHost, st));
+    MW_HIP(hipStreamSynchronize(st));
+    idx[0] = first;
+    MW_TRY(fit.scaled_rows(idx.data(), k, h_mu, h_inv, centers));
+    if (h_init_idx) std::memcpy(h_init_idx, idx.data(), k * sizeof(int64_t));
+  }
+
+  // Lloyd iterations
+  MW_HIP(hipMemsetAsync(d_labels, 255, (size_t)S, st));
+  std::vector<int64_t> q_hi((size_t)k * F, 0), q_lo((size_t)k * F, 0), count(k, 0);
+  std::vector<double> rec, cnew((size_t)k * F), weight(k), tmp(std::max(F, k));
+  int64_t last_recomputed = -1;
+  int n_iter = 0;
+  bool done = false, strict = false;
+  for (int it = 0; it < max_iter && !done; ++it) {
+    MW_TRY(fit.upload(centers));
+    int kind = 0;  // first pass
+    if (last_recomputed >= 0) {
+      double frac = (double)last_recomputed / (double)S;
+      if (fit.prev_dmax > 0.f && std::isfinite(fit.drift_max))
+        frac *= std::min(1.0, (double)fit.drift_max / (double)fit.prev_dmax);
+      kind = frac > 0.12 ? 1 : 2;
+    }
+    MW_TRY(fit.pass(0, kind, 0, rec));
+    for (size_t i = 0; i < (size_t)k * F; ++i) {
+      q_hi[i] += (int64_t)rec[i];
+      q_lo[i] += (int64_t)rec[(size_t)k * F + i];
+      const int64_t carry = q_lo[i] >> 32;
+      q_hi[i] += carry;
+      q_lo[i] -= carry << 32;
+    }
+    for (int j = 0; j < k; ++j) count[j] += (int64_t)rec[2 * (size_t)k * F + j];
+    const double* tail = rec.data() + 2 * (size_t)k * F + k;
+    const int64_t changed = (int64_t)tail[0];
+    last_recomputed = (int64_t)tail[1];
+    for (int j = 0; j < k; ++j) {
+      weight[j] = (double)count[j];
+      for (int f = 0; f < F; ++f) {
+        const size_t i = (size_t)j * F + f;
+        const double sx = ((double)q_hi[i] * 4294967296.0 + (double)q_lo[i]) * qscale[f];
+        cnew[i] = fit.a64[f] * sx + fit.b64[f] * weight[j];
+      }
+    }
+    // empty-cluster relocation (_k_means_common.pyx:181-226)
+    std::vector<int> empty;
+    for (int j = 0; j < k; ++j)
+      if (weight[j] == 0.0) empty.push_back(j);
+    if (!empty.empty()) {
+      const int ne = (int)empty.size();
+      if (!b_far.p) MW_TRY(dev_alloc<char>(b_far, mw_farthest_ws_bytes(S)));
+      MW_HIP(hipMemcpyAsync(d_c64, centers.data(), centers.size() * 8, hipMemcpyHostToDevice, st));
+      MW_TRY(mw_farthest(d_X, S, F, fit.a32, fit.b32, d_c64, k, d_labels, ne, d_topi, d_topv,
+                         b_far.p, st));
+      std::vector<int64_t> far_i(ne);
+      std::vector<double> far_v(ne);
+      MW_HIP(hipMemcpyAsync(far_i.data(), d_topi, ne * 8, hipMemcpyDeviceToHost, st));
+      MW_HIP(hipMemcpyAsync(far_v.data(), d_topv, ne * 8, hipMemcpyDeviceToHost, st));
+      MW_HIP(hipStreamSynchronize(st));
+      double vmax = far_v[0];
+      for (double v : far_v) vmax = std::max(vmax, v);
+      if (vmax != 0.0) {
+        std::vector<double> xs;
+        MW_TRY(fit.scaled_rows(far_i.data(), ne, h_mu, h_inv, xs));
+        for (int e = 0; e < ne; ++e) {
+          uint8_t old = 0;
+          MW_HIP(hipMemcpyAsync(&old, d_labels + far_i[e], 1, hipMemcpyDeviceToHost, st));
+          MW_HIP(hipStreamSynchronize(st));
+          for (int f = 0; f < F; ++f) {
+            cnew[(size_t)old * F + f] -= xs[(size_t)e * F + f];
+            cnew[(size_t)empty[e] * F + f] = xs[(size_t)e * F + f];
+          }
+          weight[empty[e]] = 1.0;
+          weight[old] -= 1.0;
+        }
+      }
+    }
+    // _average_centers (_k_means_common.pyx:229-258)
+    int amax = 0;
+    for (int j = 1; j < k; ++j)
+      if (weight[j] > weight[amax]) amax = j;
+    for (int j = 0; j < k; ++j) {
+      if (weight[j] > 0.0) {
+        const double r = 1.0 / weight[j];
+        for (int f = 0; f < F; ++f) cnew[(size_t)j * F + f] *= r;
+      } else {
+        for (int f = 0; f < F; ++f) cnew[(size_t)j * F + f] = cnew[(size_t)amax * F + f];
+      }
+    }
+    std::vector<double> shift2(k);
+    for (int j = 0; j < k; ++j) {
+      for (int f = 0; f < F; ++f) {
+        const double d = cnew[(size_t)j * F + f] - centers[(size_t)j * F + f];
+        tmp[f] = d * d;
+      }
+      const double sh = std::sqrt(np_sum(tmp.data(), F));
+      shift2[j] = sh * sh;
+    }
+    centers.swap(cnew);
+    n_iter = it + 1;
+    if (changed == 0) {
+      strict = done = true;
+    } else if (np_sum(shift2.data(), k) <= tol_abs) {
+      done = true;
+    }
+  }
+  if (!done) n_iter = max_iter;
+
+  // final pass: extra E-step unless strictly converged, and inertia
+  std::vector<double> xs2(F), cn(k);
+  for (int f = 0; f < F; ++f) {
+    const double v = std::fabs(fit.a64[f]) * (double)xmax[f] + std::fabs(fit.b64[f]);
+    xs2[f] = v * v;
+  }
+  const double xnorm = std::sqrt(np_sum(xs2.data(), F));
+  double cmax = 0.0;
+  for (int j = 0; j < k; ++j) {
+    for (int f = 0; f < F; ++f) tmp[f] = centers[(size_t)j * F + f] * centers[(size_t)j * F + f];
+    const double v = std::sqrt(np_sum(tmp.data(), F));
+    cmax = j == 0 ? v : std::max(cmax, v);
+  }
+  const double xc = xnorm + cmax;
+  const int iexp = exp_below(xc * xc * 1.01);
+  MW_TRY(fit.upload(centers));
+  MW_TRY(fit.pass(strict ? 2 : 1, 0, iexp, rec));
+  const double* tail = rec.data() + fit.rl - 4;
+  *h_inertia = (tail[2] * 4294967296.0 + tail[3]) * std::ldexp(1.0, -iexp);
+  *h_n_iter = n_iter;
+  std::memcpy(h_centers, centers.data(), centers.size() * sizeof(double));
+  return MW_OK;
+}

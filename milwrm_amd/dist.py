@@ -7,11 +7,16 @@ of a rank are its slides' subsamples, and the global row order is rank order
 is a small fixed-size message:
 
   * batch means            all-gather of (C+1) fp64 per batch, once
-  * scaler statistics      all-gather of (1+2F) fp64, Chan-merged in rank order
+  * scaler statistics      all-gather of each image's (1+2F) fp64, Chan-merged
+                           in global image order (the single-process sequence)
   * k-means++ per step     all-gather of T local potentials; all-reduce of the
                            T candidate rows (owner contributes, others zero)
-  * Lloyd per iteration    ONE all-reduce of k*F + k + 2 fp64 (sums, counts,
-                           changed labels, inertia)
+  * Lloyd fixed point      one MAX all-reduce of the F column maxima
+  * Lloyd per iteration    ONE all-reduce of the fits' records: 2kF + k + 4
+                           integer-valued fp64 limbs each (fixed-point sums,
+                           counts, changed labels, inertia) -- exact, so
+                           centers, labels and inertia are bitwise those of
+                           one process for any sharding
   * empty-cluster relocation (rare) all-gather of local top-n (dist, index)
 
 With world_size 1 every method is the identity (``LocalComm``), so the
@@ -38,6 +43,11 @@ class LocalComm:
     def merge_stats(self, stats: np.ndarray, F: int) -> np.ndarray:
         return stats
 
+    def merge_image_stats(self, per_image: np.ndarray, F: int) -> np.ndarray:
+        """[n, mean[F], M2[F]] of all images from per-image rows, Chan-merged
+        in image order (images with n = 0 contribute nothing)."""
+        return chan_merge(per_image, F)
+
     def all_reduce_(self, t: torch.Tensor):
         return t
 
@@ -56,6 +66,13 @@ def _chan(n_a, m_a, q_a, n_b, m_b, q_b):
     n = n_a + n_b
     d = m_b - m_a
     return n, m_a + d * (n_b / n), q_a + q_b + d * d * (n_a * n_b / n)
+
+
+def chan_merge(per_image: np.ndarray, F: int) -> np.ndarray:
+    n, m, q = 0.0, np.zeros(F), np.zeros(F)
+    for row in np.asarray(per_image, dtype=np.float64).reshape(-1, 1 + 2 * F):
+        n, m, q = _chan(n, m, q, row[0], row[1:1 + F], row[1 + F:])
+    return np.concatenate([[n], m, q])
 
 
 class DistComm(LocalComm):
@@ -129,6 +146,14 @@ class DistComm(LocalComm):
         dist.all_gather_object(objs, names, group=self.group)
         return set(x for o in objs for x in o)
 
+    def merge_image_stats(self, per_image: np.ndarray, F: int) -> np.ndarray:
+        """Per-image statistics of every rank (ranks hold consecutive images),
+        Chan-merged in global image order: the single-process sequence."""
+        lists = [None] * self.world
+        dist.all_gather_object(lists, np.asarray(per_image, dtype=np.float64).reshape(-1, 1 + 2 * F),
+                               group=self.group)
+        return chan_merge(np.concatenate(lists, axis=0), F)
+
     def merge_stats(self, stats: np.ndarray, F: int) -> np.ndarray:
         """Chan-merge per-rank [n, mean[F], M2[F]] in rank order."""
         g = self.all_gather_np(np.asarray(stats, dtype=np.float64))
@@ -138,46 +163,45 @@ class DistComm(LocalComm):
         return np.concatenate([[n], m, q])
 
     # -- k-means++ over row shards -------------------------------------
-    def kpp(self, rows, k, random_state, n_local_trials=None):
-        from . import _native as N
-        from . import device as D
+    def kpp(self, rows, k, random_state, n_local_trials=None, engine=None):
+        """sklearn ``_kmeans_plusplus`` (_kmeans.py:174-272) over row shards.
+        Per step: each rank's local potentials of the T trial arrays are
+        all-gathered and summed in rank order (global argmin, first wins);
+        each target ``u_t * pot`` is owned by the first rank whose prefix of
+        the best array's local potentials reaches it, and that rank searches
+        its shard for ``target - prefix``; the candidates' global indices and
+        raw rows are all-reduced (owner contributes, others zero).  ``engine``
+        holds the local distance arrays (``DeviceKpp``: the mw_kpp_* kernels;
+        tests substitute a host one)."""
         from .rng import first_center_index, kpp_draws
 
         S, F = rows.S, rows.F
+        T = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
+        eng = DeviceKpp(rows, T) if engine is None else engine
         sizes = self.all_gather_np(np.array([S], dtype=np.int64))[:, 0]
         offs = np.concatenate([[0], np.cumsum(sizes)])
         S_tot = int(offs[-1])
         off = int(offs[self.rank])
-        T = 2 + int(np.log(k)) if n_local_trials is None else int(n_local_trials)
         u0, steps = kpp_draws(random_state, k, T)
-        dev = rows.X.device
-        ws = D.WS.get("kpp", N.query("mw_kpp_ws_bytes", S, T))
-        st = D.stream()
 
         def rows_of(gidx):
             """Raw fp32 rows for global indices (owner contributes, all-reduce)."""
-            buf = torch.zeros((len(gidx), F), dtype=torch.float32, device=dev)
+            buf = eng.zeros(len(gidx))
             for i, g in enumerate(gidx):
                 if g >= 0 and off <= g < off + S:
-                    buf[i] = rows.X[g - off]
+                    buf[i] = eng.row(g - off)
             self.all_reduce_(buf)
             return buf
 
         first = first_center_index(S_tot, u0)
         chosen = [first]
         chosen_rows = [rows_of([first])[0].clone()]
-        N.call("mw_kpp_init", D.P(rows.X), S, F, D.P(rows.mu64), D.P(rows.inv64),
-               D.P(chosen_rows[0]), T, D.P(ws), st)
-        pots_dev = torch.empty(T, dtype=torch.float64, device=dev)
-        rv_dev = torch.empty(T, dtype=torch.float64, device=dev)
-        loc_dev = torch.empty(T, dtype=torch.int64, device=dev)
+        eng.init(chosen_rows[0])
         cand_g = None
         cand_rows = None
         for c in range(1, k + 1):
             n_arr = 1 if c == 1 else T
-            N.call("mw_kpp_pots", D.P(ws), S, T, c, D.P(pots_dev), st)
-            local = pots_dev[:n_arr].cpu().numpy()
-            g = self.all_gather_np(local)  # [world, n_arr]
+            g = self.all_gather_np(eng.pots(c, n_arr))  # [world, n_arr]
             tot = np.zeros(n_arr)
             for r in range(self.world):
                 tot = tot + g[r]
@@ -187,58 +211,41 @@ class DistComm(LocalComm):
                 chosen_rows.append(cand_rows[best].clone())
             if c == k:
                 break
-            pot = tot[best]
-            rv = np.asarray(steps[c - 1], dtype=np.float64) * pot
-            pre = np.concatenate([[0.0], np.cumsum(g[:, best])])
-            rv_local = np.full(T, -1.0)
-            for t in range(T):
-                owner = self.world - 1
-                for r in range(self.world):
-                    if pre[r + 1] >= rv[t]:
-                        owner = r
-                        break
-                if owner == self.rank:
-                    rv_local[t] = max(rv[t] - pre[owner], 0.0)
-            rv_dev.copy_(torch.from_numpy(rv_local))
-            N.call("mw_kpp_search", D.P(ws), S, T, c, best, D.P(rv_dev), D.P(loc_dev), st)
-            loc = loc_dev.cpu().numpy()
-            gl = np.where(loc >= 0, loc + off, 0).astype(np.int64)
-            gsum = torch.from_numpy(gl).to(dev)
+            rv_local = kpp_targets(np.asarray(steps[c - 1], dtype=np.float64) * tot[best],
+                                   g[:, best], self.rank)
+            loc = eng.search(c, best, rv_local)
+            gsum = torch.from_numpy(np.where(loc >= 0, loc + off, 0).astype(np.int64))
             self.all_reduce_(gsum)
-            cand_g = gsum.cpu().numpy()
-            buf = torch.zeros((T, F), dtype=torch.float32, device=dev)
+            cand_g = gsum.numpy()
+            buf = eng.zeros(T)
             for t in range(T):
                 if loc[t] >= 0:
-                    buf[t] = rows.X[int(loc[t])]
+                    buf[t] = eng.row(int(loc[t]))
             self.all_reduce_(buf)
             cand_rows = buf
-            N.call("mw_kpp_trial", D.P(rows.X), S, F, D.P(rows.mu64), D.P(rows.inv64), c, best,
-                   D.P(buf), T, D.P(ws), st)
+            eng.trial(c, best, buf)
         X0 = torch.stack(chosen_rows).double().cpu().numpy()
         return (X0 - rows.mu) * rows.inv, np.asarray(chosen, dtype=np.int64)
 
     # -- empty-cluster relocation --------------------------------------
-    def farthest(self, rows, labels, centers_old, n):
-        from . import _native as N
-        from . import device as D
-
+    def farthest(self, rows, labels, centers_old, n, local_top=None):
+        """The n rows farthest from their own center over all shards
+        (_relocate_empty_clusters_dense's argpartition, _k_means_common.pyx:
+        181-226): each rank's local top n (``mw_farthest``; ``local_top(m)``
+        -> (values, local indices) substitutes it in tests) are all-gathered
+        and ordered by (distance desc, global index asc); the winners' raw
+        rows and labels are all-reduced from their owners.  Returns (global
+        indices, distances, scaled rows, old labels)."""
         S, F = rows.S, rows.F
-        k = centers_old.shape[0]
         dev = rows.X.device
         sizes = self.all_gather_np(np.array([S], dtype=np.int64))[:, 0]
         off = int(np.concatenate([[0], np.cumsum(sizes)])[self.rank])
-        c64 = torch.from_numpy(np.ascontiguousarray(centers_old)).to(dev)
         m = min(n, S)
-        top_i = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
-        top_v = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
-        if m > 0:
-            ws = D.WS.get("far", N.query("mw_farthest_ws_bytes", S))
-            N.call("mw_farthest", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(c64), k,
-                   D.P(labels), int(m), D.P(top_i), D.P(top_v), D.P(ws), D.stream())
         vi = np.full((n, 2), -1.0)
         if m > 0:
-            vi[:m, 0] = top_v[:m].cpu().numpy()
-            vi[:m, 1] = top_i[:m].cpu().numpy() + off
+            top_v, top_i = (local_top or _device_far(rows, labels, centers_old))(m)
+            vi[:m, 0] = top_v[:m]
+            vi[:m, 1] = top_i[:m] + off
         g = self.all_gather_np(vi).reshape(-1, 2)
         g = g[g[:, 1] >= 0]
         order = np.lexsort((g[:, 1], -g[:, 0]))[:n]
@@ -255,6 +262,88 @@ class DistComm(LocalComm):
         b = buf.cpu().numpy()
         xs = (b[:, :F] - rows.mu) * rows.inv
         return far_idx, far_val, xs, b[:, F].astype(np.int64)
+
+
+def _device_far(rows, labels, centers_old):
+    def top(m):
+        from . import _native as N
+        from . import device as D
+
+        dev = rows.X.device
+        c64 = torch.from_numpy(np.ascontiguousarray(centers_old)).to(dev)
+        top_i = torch.empty(m, dtype=torch.int64, device=dev)
+        top_v = torch.empty(m, dtype=torch.float64, device=dev)
+        ws = D.WS.get("far", N.query("mw_farthest_ws_bytes", rows.S))
+        N.call("mw_farthest", D.P(rows.X), rows.S, rows.F, D.P(rows.a32), D.P(rows.b32), D.P(c64),
+               centers_old.shape[0], D.P(labels), int(m), D.P(top_i), D.P(top_v), D.P(ws),
+               D.stream())
+        return top_v.cpu().numpy(), top_i.cpu().numpy()
+    return top
+
+
+def kpp_targets(rv, local_pots, rank):
+    """Local search targets of this rank: target t belongs to the first rank
+    whose inclusive prefix of local potentials (rank order) reaches rv[t]
+    (the last rank if rounding leaves it unreached) and is searched there
+    for rv[t] - prefix; -1 on every other rank."""
+    pre = np.concatenate([[0.0], np.cumsum(local_pots)])
+    world = len(local_pots)
+    out = np.full(len(rv), -1.0)
+    for t, v in enumerate(rv):
+        owner = world - 1
+        for r in range(world):
+            if pre[r + 1] >= v:
+                owner = r
+                break
+        if owner == rank:
+            out[t] = max(v - pre[owner], 0.0)
+    return out
+
+
+class DeviceKpp:
+    """Local k-means++ state of one shard on the device (mw_kpp_* kernels):
+    the ping-pong banks of T candidate-min distance arrays and their
+    per-block sums live in the kernel workspace."""
+
+    def __init__(self, rows, T):
+        from . import _native as N
+        from . import device as D
+
+        self.N, self.D, self.rows, self.T = N, D, rows, T
+        self.ws = D.WS.get("kpp", N.query("mw_kpp_ws_bytes", rows.S, T))
+        dev = rows.X.device
+        self.pots_dev = torch.empty(T, dtype=torch.float64, device=dev)
+        self.rv_dev = torch.empty(T, dtype=torch.float64, device=dev)
+        self.loc_dev = torch.empty(T, dtype=torch.int64, device=dev)
+
+    def zeros(self, n):
+        return torch.zeros((n, self.rows.F), dtype=torch.float32, device=self.rows.X.device)
+
+    def row(self, i):
+        return self.rows.X[i]
+
+    def init(self, center_row):
+        r, D = self.rows, self.D
+        self.N.call("mw_kpp_init", D.P(r.X), r.S, r.F, D.P(r.mu64), D.P(r.inv64), D.P(center_row),
+                    self.T, D.P(self.ws), D.stream())
+
+    def pots(self, c, n_arr):
+        D = self.D
+        self.N.call("mw_kpp_pots", D.P(self.ws), self.rows.S, self.T, c, D.P(self.pots_dev),
+                    D.stream())
+        return self.pots_dev[:n_arr].cpu().numpy()
+
+    def search(self, c, best, rv_local):
+        D = self.D
+        self.rv_dev.copy_(torch.from_numpy(rv_local))
+        self.N.call("mw_kpp_search", D.P(self.ws), self.rows.S, self.T, c, best, D.P(self.rv_dev),
+                    D.P(self.loc_dev), D.stream())
+        return self.loc_dev.cpu().numpy()
+
+    def trial(self, c, best, cand_rows):
+        r, D = self.rows, self.D
+        self.N.call("mw_kpp_trial", D.P(r.X), r.S, r.F, D.P(r.mu64), D.P(r.inv64), c, best,
+                    D.P(cand_rows), self.T, D.P(self.ws), D.stream())
 
 
 LOCAL_COMM = LocalComm()

@@ -61,3 +61,155 @@ def test_gloo_world2_collectives():
         np.testing.assert_allclose(merged[6:] / 237, X.var(0), rtol=1e-12)
         assert e == [30.0, 40.0] and p == 15
         assert sb["a"] == ([3.0, 4.0], 7.0) and sb["b"] == ([5.0, 6.0], 9.0)
+
+
+class _HostRows:
+    """Stand-in for DeviceRows on CPU: raw fp32 rows + the scaler affine."""
+
+    def __init__(self, X, mu, inv):
+        import torch
+
+        self.X = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32))
+        self.S, self.F = X.shape
+        self.mu, self.inv = mu, inv
+
+    def scaled(self):
+        return (self.X.double().numpy() - self.mu) * self.inv
+
+
+class _HostKpp:
+    """Host engine with the semantics of the mw_kpp_* kernels (oracle-style
+    squared distances in fp64, sequential cumsum search, first-reach)."""
+
+    def __init__(self, rows, T):
+        self.rows, self.T = rows, T
+        self.Xs = rows.scaled()
+        self.bank = None
+
+    def zeros(self, n):
+        import torch
+
+        return torch.zeros((n, self.rows.F), dtype=torch.float32)
+
+    def row(self, i):
+        return self.rows.X[i]
+
+    def _d2(self, raw):
+        c = (raw.double().numpy() - self.rows.mu) * self.rows.inv
+        return ((self.Xs - c) ** 2).sum(1)
+
+    def init(self, center_row):
+        self.bank = [self._d2(center_row)]
+
+    def pots(self, c, n_arr):
+        return np.array([self.bank[i].sum() for i in range(n_arr)])
+
+    def search(self, c, best, rv_local):
+        cum = np.cumsum(self.bank[best])
+        out = np.full(self.T, -1, dtype=np.int64)
+        for t, rv in enumerate(rv_local):
+            if rv >= 0:
+                out[t] = min(int(np.searchsorted(cum, rv)), self.rows.S - 1)
+        return out
+
+    def trial(self, c, best, cand_rows):
+        base = self.bank[best]
+        self.bank = [np.minimum(base, self._d2(cand_rows[t])) for t in range(self.T)]
+
+
+def _kpp_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from milwrm_amd.dist import DistComm
+
+        comm = DistComm(device=__import__("torch").device("cpu"))
+        X, mu, inv, cuts = _kpp_data(world)
+        rows = _HostRows(X[cuts[rank]:cuts[rank + 1]], mu, inv)
+        res = {}
+        for k in (2, 6, 13):
+            _, idx = comm.kpp(rows, k, 18, engine=_HostKpp(rows, 2 + int(np.log(k))))
+            res[k] = idx
+        # farthest-row merge with a host local top-n (distance to own center)
+        lab = np.arange(rows.S) % 3
+        cents = np.stack([X[i::3].mean(0) for i in range(3)])
+        cs = (cents - mu) * inv
+        d = ((rows.scaled() - cs[lab]) ** 2).sum(1)
+
+        def local_top(m):
+            o = np.lexsort((np.arange(rows.S), -d))[:m]
+            return d[o], o
+
+        import torch
+
+        far = comm.farthest(rows, torch.from_numpy(lab), cs, 4, local_top=local_top)
+        res["far"] = (far[0], far[1], far[2], far[3])
+        res["img_stats"] = comm.merge_image_stats(_img_stats()[[0, 1] if rank == 0 else [2, 3, 4]], 3)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _img_stats():
+    rng = np.random.default_rng(4)
+    out = []
+    for i in range(5):
+        Y = rng.normal(i, 1 + i, size=(0 if i == 3 else 50 + 13 * i, 3))
+        n = Y.shape[0]
+        out.append(np.concatenate([[n], Y.mean(0) if n else np.zeros(3),
+                                   Y.var(0) * n if n else np.zeros(3)]))
+    return np.array(out)
+
+
+def _kpp_data(world):
+    rng = np.random.default_rng(11)
+    cents = rng.normal(0, 3, size=(9, 4))
+    X = (cents[rng.integers(0, 9, 900)] + rng.normal(0, 1, size=(900, 4))).astype(np.float32)
+    mu = X.astype(np.float64).mean(0)
+    inv = 1.0 / X.astype(np.float64).std(0)
+    cuts = [0, 389, 900] if world == 2 else [0, 900]
+    return X, mu, inv, cuts
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_kpp_and_farthest_merge():
+    """DistComm.kpp's target ownership / global argmin over 2 shards (host
+    engine with the kernels' semantics) gives sklearn's k-means++ indices on
+    the whole row set (oracle), and the farthest-row merge returns the
+    global top n with the owners' rows and labels."""
+    from oracle import milwrm_oracle as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_kpp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=90) for _ in ps)
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    X, mu, inv, cuts = _kpp_data(2)
+    Xs = (X.astype(np.float64) - mu) * inv
+    for k in (2, 6, 13):
+        _, ref = O.kmeans_plusplus(Xs, k, 18)
+        np.testing.assert_array_equal(res[0][k], ref)
+        np.testing.assert_array_equal(res[1][k], ref)
+    from milwrm_amd.dist import LOCAL_COMM
+
+    single = LOCAL_COMM.merge_image_stats(_img_stats(), 3)  # bitwise the one-process merge
+    np.testing.assert_array_equal(res[0]["img_stats"], single)
+    np.testing.assert_array_equal(res[1]["img_stats"], single)
+    lab = np.concatenate([np.arange(cuts[r + 1] - cuts[r]) % 3 for r in range(2)])
+    cents = np.stack([X[i::3].mean(0) for i in range(3)])
+    cs = (cents - mu) * inv
+    d = ((Xs - cs[lab]) ** 2).sum(1)
+    want = np.lexsort((np.arange(900), -d))[:4]
+    for r in (0, 1):
+        idx, val, xs, old = res[r]["far"]
+        np.testing.assert_array_equal(idx, want)
+        np.testing.assert_allclose(val, d[want], rtol=1e-12)
+        np.testing.assert_allclose(xs, Xs[want], rtol=1e-12)
+        np.testing.assert_array_equal(old, lab[want])
