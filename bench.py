@@ -184,7 +184,10 @@ def main():
     n_iter = int(lab.kmeans.n_iter_)
     S = int(lab._rows.S)
     # dominant kernel by device time inside the timed region
-    dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["total_ms"])
+    # (timed regions without an algorithmic byte count, e.g. the whole k-means
+    # fit in the C++ driver, are not kernels with a roofline)
+    dom_name, dom = max(((n, r) for n, r in prof.items() if r["bytes"] > 0),
+                        key=lambda kv: kv[1]["total_ms"])
     per_launch_bytes = dom["bytes"] / max(dom["count"], 1)
     achieved = per_launch_bytes / (dom["mean_ms"] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom_name)

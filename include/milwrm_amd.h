@@ -134,6 +134,11 @@ int mw_sample_fixup(const int32_t* d_pix, const int32_t* d_head, int64_t S, int 
  * the workspace of each; merged in call order. */
 int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats,
                           int accumulate, void* stream);
+/* Column max |x| of the same rows (fp32 d_out[F]; maxed into d_out when
+ * accumulating): the fixed-point exponents of mw_lloyd_pass come from it
+ * (replaces a separate mw_col_absmax pass over the rows). */
+int mw_col_stats_absmax(const void* d_ws, int64_t S, int F, float* d_out, int accumulate,
+                        void* stream);
 
 /* ---- legacy MT19937 subsample indices (MxIF.py:484,490) ---------------------
  * Bit-exact np.random.RandomState(seed).randint(0, high, size) (== choice),
@@ -169,6 +174,9 @@ int mw_legacy_randint_from_states(const uint32_t* d_states, int64_t W_avail, int
 
 /* ---- k-means++ (sklearn _kmeans.py:174-272) ---------------------------------
  * Rows are scaled on the fly: x' = (x - mu) * inv_sigma  (fp64 affine).
+ * The workspace keeps the closest distance of every row (fp64) and per-block
+ * / per-64-row-tile sums of the step's T trial arrays (the arrays themselves
+ * are recomputed where the search needs them, never stored).
  * Single device: mw_kpp_init + (k-1) x mw_kpp_step + mw_kpp_indices keep all
  * state on the device (no host synchronisation between steps).
  * Row-sharded (one shard per rank): mw_kpp_init, then per step c
@@ -190,12 +198,13 @@ int mw_kpp_indices(const void* d_ws, int64_t S, int T, int k, int64_t* d_idx_out
 /* sharded: local potentials (fp64) of the arrays finished before step c
  * (1 array after init, T after a trial) */
 int mw_kpp_pots(const void* d_ws, int64_t S, int T, int c, double* d_pots, void* stream);
-/* sharded: search array `best` of step c-1 for local targets d_rv[T] (fp64,
- * < 0 = not on this shard); local row indices (int64, -1 if skipped) */
-int mw_kpp_search(void* d_ws, int64_t S, int T, int c, int best, const double* d_rv,
-                  int64_t* d_local_idx, void* stream);
-/* sharded: trial pass of step c against candidate rows d_rows (T x F raw
- * fp32), minimum taken with array `best` of step c-1 */
+/* sharded: search array `best` of step c-1 (recomputed from the rows where
+ * needed) for local targets d_rv[T] (fp64, < 0 = not on this shard); local
+ * row indices (int64, -1 if skipped) */
+int mw_kpp_search(const float* d_X, int64_t S, int F, void* d_ws, int T, int c, int best,
+                  const double* d_rv, int64_t* d_local_idx, void* stream);
+/* sharded: pass of step c against candidate rows d_rows (T x F raw fp32),
+ * after folding in array `best` of step c-1 */
 int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu,
                  const double* d_inv, int c, int best, const float* d_rows, int T,
                  void* d_ws, void* stream);
@@ -253,24 +262,28 @@ int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream
 /* ---- whole fit: sklearn KMeans(algorithm="lloyd").fit (_kmeans.py:1427-1554)
  * Replaces the reference's `KMeans(n_clusters=k, random_state=seed).fit(X)`
  * (MILWRM.py:706-737 find_tissue_regions; MILWRM.py:29-54 kMeansRes) for a
- * caller of the C ABI.  Rows: S x F raw fp32 on the device, scaled on the fly
- * x' = (x - mu) * inv (fp64 host arrays; pass mu = 0, inv = 1 for rows that
- * are already standardised).  k-means++ seeded from RandomState(seed) (or the
- * k x F scaled centers h_init, then no seeding), Lloyd with sklearn's strict
- * and tolerance convergence (tol relative: tol * mean of the scaled rows'
- * per-feature variance, taken from h_feature_var[F] when given, else computed
- * on the device), empty-cluster relocation, the extra E-step and inertia.
+ * caller of the C ABI; KMeans.fit of the Python package runs through it too
+ * (single process, one k-means++ init from an int seed or an explicit init).
+ * Rows: S x F raw fp32 on the device, scaled on the fly x' = (x - mu) * inv
+ * (fp64 host arrays; mu = 0, inv = 1 for rows that are already standardised).
+ * k-means++ seeded from RandomState(seed) (or the k x F scaled centers
+ * h_init, then no seeding), Lloyd with sklearn's strict and tolerance
+ * convergence (tol relative: tol * mean of the scaled rows' per-feature
+ * variance, from h_feature_var[F] when given, else computed on the device),
+ * empty-cluster relocation, the extra E-step and inertia.  h_xmax[F]: the
+ * rows' column max |x| when the producer already has it (else one pass).
  * Outputs: d_labels (S uint8, device), h_centers (k x F fp64, scaled space),
  * *h_inertia, *h_n_iter, h_init_idx (k int64, may be NULL; untouched with
- * h_init).  Same numbers as the Python KMeans.fit on the same rows.  Caps:
- * 1 <= k <= 64 (labels are uint8, centers live in LDS), 1 <= F <= 64 (one
- * feature per lane of a wave); S >= k.  Allocates and frees its own device
- * workspace; synchronises `stream` before returning. */
+ * h_init).  d_ws: mw_kmeans_fit_ws_bytes(S, F, k) bytes of device workspace
+ * (NULL: allocated and freed inside).  Caps: 1 <= k <= 64 (uint8 labels,
+ * centers in LDS / scalar registers), 1 <= F <= 64 (one feature per lane of
+ * a wave); S >= k.  Synchronises `stream` before returning. */
+size_t mw_kmeans_fit_ws_bytes(int64_t S, int F, int k);
 int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
-                  const double* h_inv, const double* h_feature_var, int k,
-                  const double* h_init, uint32_t seed, int max_iter, double tol,
+                  const double* h_inv, const double* h_feature_var, const float* h_xmax,
+                  int k, const double* h_init, uint32_t seed, int max_iter, double tol,
                   uint8_t* d_labels, double* h_centers, double* h_inertia, int* h_n_iter,
-                  int64_t* h_init_idx, void* stream);
+                  int64_t* h_init_idx, void* d_ws, size_t ws_bytes, void* stream);
 
 /* ---- empty-cluster relocation support (_k_means_common.pyx:181-226) ---------
  * fp64 distance of every row to centers[labels]; returns the n largest

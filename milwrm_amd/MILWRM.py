@@ -449,6 +449,7 @@ class mxif_labeler(tissue_labeler):
         # image order (comm.merge_image_stats): the same merge sequence for any
         # sharding of the images over ranks, so the scaler is bitwise the same
         img_stats = torch.zeros((len(images), 1 + 2 * F), dtype=torch.float64, device=dev)
+        xmax = torch.zeros(F, dtype=torch.float32, device=dev)  # column max |x| (Lloyd fixed point)
         # phase 2: fused lognorm+blur, gather rows into X (image_df order)
         off = 0
         paths = []
@@ -463,10 +464,11 @@ class mxif_labeler(tissue_labeler):
                 totals.append((tot, S))
                 feat = D.h2d(np.asarray(im._features(features), dtype=np.int32), dev)
                 if _gather_deferred(im, feat, idx, r2p, X[off:off + S]):
-                    D.col_stats_rows(X[off:off + S], img_stats[n_img], accumulate=False)
+                    D.col_stats_rows(X[off:off + S], img_stats[n_img], accumulate=False,
+                                     absmax=xmax)
                 else:
                     D.gather_rows(D.as_float32(im._materialize()), feat, idx, r2p, X[off:off + S],
-                                  img_stats[n_img], accumulate=False)
+                                  img_stats[n_img], accumulate=False, absmax=xmax)
             off += S
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))
@@ -480,7 +482,8 @@ class mxif_labeler(tissue_labeler):
         st = comm.merge_image_stats(D.d2h(img_stats), F)
         self.scaler = StandardScaler.from_stats(st)
         mu, inv = self.scaler.affine()
-        self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv)
+        self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv,
+                                xmax_local=D.d2h(xmax))
         self._cluster_host = None
 
     def _image_list(self):

@@ -57,14 +57,15 @@ _PROTOS = {
     "mw_kpp_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_kpp_indices": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mw_kpp_pots": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
-    "mw_kpp_search": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "mw_kpp_search": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "mw_kpp_trial": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_lloyd_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "mw_lloyd_rec_len": (c_i32, [c_i32, c_i32]),
     "mw_lloyd_pass": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "mw_col_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
-    "mw_kmeans_fit": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_u32, c_i32,
-                              C.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mw_kmeans_fit_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
+    "mw_kmeans_fit": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_u32, c_i32,
+                              C.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "mw_farthest_ws_bytes": (c_sz, [c_i64]),
     "mw_farthest": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_ws_bytes": (c_sz, [c_i64, c_i32]),
@@ -74,6 +75,7 @@ _PROTOS = {
     "mw_domain_sse": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "mw_neighbor_mean": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_col_stats_rows": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_col_stats_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),
     "mw_sample_head_elems": (c_sz, [c_i64]),
     "mw_sample_map": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mw_blur_sample": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -74,18 +74,60 @@ double np_sum(const double* a, int64_t n) {
   return np_sum(a, n2) + np_sum(a + n2, n - n2);
 }
 
-// RandomState.choice(n, p=ones(n)/n) given its uniform draw u
-// (cdf = sequential cumsum of 1/n, normalised by its last entry,
-// searchsorted 'right')
+// RandomState.choice(n, p=ones(n)/n) given its uniform draw u: cdf = the
+// sequential cumsum of c = 1/n, normalised by its last entry, searchsorted
+// 'right'.  Inside a binade the running sum advances by a constant increment
+// (after one explicit step that fixes the rounding parity), so the sum is
+// evaluated run by run (rng.py _runs / _s_at, the same fp64 operations).
+struct CdfRun {
+  int64_t i0;
+  double s0, inc;
+  int64_t m;
+};
+static std::vector<CdfRun> cdf_runs(int64_t n) {
+  std::vector<CdfRun> runs;
+  const double c = 1.0 / (double)n;
+  int64_t i = 0;
+  double s = c;
+  while (i < n) {
+    runs.push_back({i, s, 0.0, 1});
+    i += 1;
+    if (i >= n) break;
+    const double t = s + c;
+    const double u = t + c;
+    const double inc = u - t;
+    int m_exp;
+    std::frexp(t, &m_exp);
+    const double top = std::ldexp(1.0, m_exp);
+    int64_t m;
+    if (inc > 0) {
+      int64_t j = (int64_t)((top - t) / inc);
+      while (j > 0 && t + (double)j * inc >= top) --j;
+      while (t + (double)(j + 1) * inc < top) ++j;
+      m = std::min(j + 1, n - i);
+    } else {
+      m = n - i;
+    }
+    runs.push_back({i, t, inc, m});
+    i += m;
+    s = (t + (double)(m - 1) * inc) + c;
+  }
+  return runs;
+}
 int64_t first_center_index(int64_t n, double u) {
-  const double p = 1.0 / (double)n;
-  double s = 0.0;
-  for (int64_t i = 0; i < n; ++i) s += p;
-  const double total = s;
-  s = 0.0;
-  for (int64_t i = 0; i < n; ++i) {
-    s += p;
-    if (s / total > u) return i;
+  const std::vector<CdfRun> runs = cdf_runs(n);
+  const CdfRun& last = runs.back();
+  const double total = last.s0 + (double)(last.m - 1) * last.inc;
+  for (const CdfRun& r : runs) {
+    if ((r.s0 + (double)(r.m - 1) * r.inc) / total > u) {
+      int64_t lo = 0, hi = r.m - 1;  // first j with s_j / total > u
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) / 2;
+        if ((r.s0 + (double)mid * r.inc) / total > u) hi = mid;
+        else lo = mid + 1;
+      }
+      return r.i0 + lo;
+    }
   }
   return n;
 }
@@ -140,8 +182,9 @@ struct Fit {
 
   // centers / drift / half-separation tables of the next pass (kmeans.py
   // _bound_tables; the values only steer which rows skip the E-step)
+  std::vector<float> h;  // staging of the uploaded tables (outlives the async copy)
   int upload(const std::vector<double>& c) {
-    std::vector<float> h((size_t)k * F + 2 * k);
+    h.assign((size_t)k * F + 2 * k, 0.f);
     for (size_t i = 0; i < (size_t)k * F; ++i) h[i] = (float)c[i];
     std::vector<double> drift(k, 0.0), half(k, std::numeric_limits<double>::infinity()), tmp(F);
     for (int j = 0; j < k; ++j) {
@@ -203,27 +246,58 @@ struct Fit {
   // raw rows idx[i] -> scaled fp64 (x - mu) * inv
   int scaled_rows(const int64_t* idx, int n, const double* mu, const double* inv,
                   std::vector<double>& outv) {
-    std::vector<float> r((size_t)F);
+    std::vector<float> r((size_t)n * F);
     outv.resize((size_t)n * F);
-    for (int i = 0; i < n; ++i) {
-      MW_HIP(hipMemcpyAsync(r.data(), X + idx[i] * F, F * sizeof(float), hipMemcpyDeviceToHost, st));
-      MW_HIP(hipStreamSynchronize(st));
-      for (int f = 0; f < F; ++f) outv[(size_t)i * F + f] = ((double)r[f] - mu[f]) * inv[f];
-    }
+    for (int i = 0; i < n; ++i)
+      MW_HIP(hipMemcpyAsync(r.data() + (size_t)i * F, X + idx[i] * F, F * sizeof(float),
+                            hipMemcpyDeviceToHost, st));
+    MW_HIP(hipStreamSynchronize(st));
+    for (int i = 0; i < n; ++i)
+      for (int f = 0; f < F; ++f)
+        outv[(size_t)i * F + f] = ((double)r[(size_t)i * F + f] - mu[f]) * inv[f];
     return MW_OK;
   }
 };
+
+// Workspace (256-aligned sections): small arrays | par | ub | lb | Lloyd
+// records | out | one region shared by the column statistics (tolerance),
+// the k-means++ state and the relocation scratch (never live together).
+struct FitLayout {
+  size_t small, par, ub, lb, lws, out, big, total;
+};
+static inline size_t fal(size_t x) { return (x + 255) & ~(size_t)255; }
+static FitLayout fit_layout(int64_t S, int F, int k) {
+  const int T = 2 + (int)std::log((double)(k < 1 ? 1 : k));
+  FitLayout L;
+  L.small = 0;
+  L.par = fal(64 * 4 * 4 + 64 * 8 * 2 + 64 * 64 * 8 + 64 * 8 * 2 + 130 * 8 + 64 * 8);
+  L.ub = L.par + fal(((size_t)k * F + 2 * k) * 4);
+  L.lb = L.ub + fal((size_t)S * 4);
+  L.lws = L.lb + fal((size_t)S * 4);
+  L.out = L.lws + fal(mw_lloyd_ws_bytes(S, k, F));
+  L.big = L.out + fal((size_t)mw_lloyd_rec_len(k, F) * 8);
+  size_t big = mw_gather_ws_bytes(S, F);
+  if (T <= 8) big = std::max(big, mw_kpp_ws_bytes(S, T));
+  big = std::max(big, mw_farthest_ws_bytes(S));
+  L.total = L.big + fal(big);
+  return L;
+}
 
 }  // namespace
 }  // namespace mw
 
 using namespace mw;
 
+extern "C" size_t mw_kmeans_fit_ws_bytes(int64_t S, int F, int k) {
+  if (S <= 0 || F < 1 || F > 64 || k < 1 || k > 64) return 0;
+  return fit_layout(S, F, k).total;
+}
+
 extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
-                             const double* h_inv, const double* h_feature_var, int k,
-                             const double* h_init, uint32_t seed, int max_iter, double tol,
+                             const double* h_inv, const double* h_feature_var, const float* h_xmax,
+                             int k, const double* h_init, uint32_t seed, int max_iter, double tol,
                              uint8_t* d_labels, double* h_centers, double* h_inertia, int* h_n_iter,
-                             int64_t* h_init_idx, void* stream) {
+                             int64_t* h_init_idx, void* d_ws, size_t ws_bytes, void* stream) {
   MW_CHECK_ARG(d_X && h_mu && h_inv && d_labels && h_centers && h_inertia && h_n_iter,
                "mw_kmeans_fit: null pointer");
   MW_CHECK_ARG(F >= 1 && F <= 64, "mw_kmeans_fit: F=%d outside [1, 64]", F);
@@ -232,7 +306,16 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
   MW_CHECK_ARG(max_iter >= 1 && tol >= 0.0, "mw_kmeans_fit: bad max_iter / tol");
   const int T = 2 + (int)std::log((double)k);
   MW_CHECK_ARG(h_init || T <= 8, "mw_kmeans_fit: n_local_trials > 8");
+  const FitLayout L = fit_layout(S, F, k);
+  MW_CHECK_ARG(!d_ws || ws_bytes >= L.total, "mw_kmeans_fit: workspace %zu < %zu bytes", ws_bytes,
+               L.total);
   hipStream_t st = as_stream(stream);
+  DevBuf own;
+  if (!d_ws) {
+    MW_TRY(dev_alloc<char>(own, L.total));
+    d_ws = own.p;
+  }
+  char* base = static_cast<char*>(d_ws);
 
   Fit fit;
   fit.S = S;
@@ -241,11 +324,9 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
   fit.st = st;
   fit.X = d_X;
   fit.rl = mw_lloyd_rec_len(k, F);
-  DevBuf b_small, b_par, b_ub, b_lb, b_ws, b_out, b_kpp, b_far, b_idx, b_cs;
-  // small: a32[F] b32[F] qexp[F] absmax[F] mu64[F] inv64[F] c64[k F] topv[64] topi[64] stats[1+2F]
-  const size_t small = 4 * 64 * 4 + 2 * 64 * 8 + 64 * 64 * 8 + 64 * 8 + 64 * 8 + 130 * 8;
-  MW_TRY(dev_alloc<char>(b_small, small));
-  char* sp = reinterpret_cast<char*>(b_small.p);
+  // small: a32[64] b32[64] qexp[64] absmax[64] | mu64[64] inv64[64] | c64[64 x 64] |
+  //        topv[64] topi[64] | stats[130] | idx[64]
+  char* sp = base + L.small;
   fit.a32 = reinterpret_cast<float*>(sp);
   fit.b32 = fit.a32 + 64;
   fit.qexp = reinterpret_cast<int32_t*>(fit.b32 + 64);
@@ -256,16 +337,13 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
   double* d_topv = d_c64 + 64 * 64;
   int64_t* d_topi = reinterpret_cast<int64_t*>(d_topv + 64);
   double* d_stats = reinterpret_cast<double*>(d_topi + 64);
-  MW_TRY(dev_alloc<float>(b_par, (size_t)k * F + 2 * k));
-  fit.par = reinterpret_cast<float*>(b_par.p);
-  MW_TRY(dev_alloc<float>(b_ub, S));
-  MW_TRY(dev_alloc<float>(b_lb, S));
-  fit.ub = reinterpret_cast<float*>(b_ub.p);
-  fit.lb = reinterpret_cast<float*>(b_lb.p);
-  MW_TRY(dev_alloc<char>(b_ws, mw_lloyd_ws_bytes(S, k, F)));
-  fit.ws = b_ws.p;
-  MW_TRY(dev_alloc<double>(b_out, fit.rl));
-  fit.out = reinterpret_cast<double*>(b_out.p);
+  int64_t* d_idx = reinterpret_cast<int64_t*>(d_stats + 130);
+  fit.par = reinterpret_cast<float*>(base + L.par);
+  fit.ub = reinterpret_cast<float*>(base + L.ub);
+  fit.lb = reinterpret_cast<float*>(base + L.lb);
+  fit.ws = base + L.lws;
+  fit.out = reinterpret_cast<double*>(base + L.out);
+  void* big = base + L.big;
   fit.labels = d_labels;
 
   // folded scaler: x' = x * a + b (fp32), as DeviceRows
@@ -290,10 +368,8 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
     if (h_feature_var) {
       for (int f = 0; f < F; ++f) var[f] = h_feature_var[f];
     } else {
-      DevBuf b_g;
-      MW_TRY(dev_alloc<char>(b_g, mw_gather_ws_bytes(S, F)));
-      MW_TRY(mw_col_stats_rows(d_X, S, F, b_g.p, st));
-      MW_TRY(mw_col_stats_finalize(b_g.p, S, F, d_stats, 0, st));
+      MW_TRY(mw_col_stats_rows(d_X, S, F, big, st));
+      MW_TRY(mw_col_stats_finalize(big, S, F, d_stats, 0, st));
       std::vector<double> hs(1 + 2 * F);
       MW_HIP(hipMemcpyAsync(hs.data(), d_stats, hs.size() * 8, hipMemcpyDeviceToHost, st));
       MW_HIP(hipStreamSynchronize(st));
@@ -303,10 +379,14 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
   }
 
   // fixed-point exponents of the M-step from the column max |x|
-  MW_TRY(mw_col_absmax(d_X, S, F, d_absmax, st));
   std::vector<float> xmax(F);
-  MW_HIP(hipMemcpyAsync(xmax.data(), d_absmax, F * 4, hipMemcpyDeviceToHost, st));
-  MW_HIP(hipStreamSynchronize(st));
+  if (h_xmax) {  // taken beside the scaler statistics by the producer of the rows
+    for (int f = 0; f < F; ++f) xmax[f] = h_xmax[f];
+  } else {
+    MW_TRY(mw_col_absmax(d_X, S, F, d_absmax, st));
+    MW_HIP(hipMemcpyAsync(xmax.data(), d_absmax, F * 4, hipMemcpyDeviceToHost, st));
+    MW_HIP(hipStreamSynchronize(st));
+  }
   std::vector<int32_t> qe(F);
   std::vector<double> qscale(F);
   for (int f = 0; f < F; ++f) {
@@ -323,17 +403,15 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
     LegacyRandom rs(seed);
     const double u0 = rs.sample();
     const int64_t first = first_center_index(S, u0);
-    MW_TRY(dev_alloc<char>(b_kpp, mw_kpp_ws_bytes(S, T)));
-    MW_TRY(mw_kpp_init(d_X, S, F, d_mu, d_inv, d_X + first * F, T, b_kpp.p, st));
+    MW_TRY(mw_kpp_init(d_X, S, F, d_mu, d_inv, d_X + first * F, T, big, st));
     std::vector<double> u(T);
     for (int c = 1; c < k; ++c) {
       for (int t = 0; t < T; ++t) u[t] = rs.sample();
-      MW_TRY(mw_kpp_step(d_X, S, F, d_mu, d_inv, c, u.data(), T, b_kpp.p, st));
+      MW_TRY(mw_kpp_step(d_X, S, F, d_mu, d_inv, c, u.data(), T, big, st));
     }
-    MW_TRY(dev_alloc<int64_t>(b_idx, k));
-    MW_TRY(mw_kpp_indices(b_kpp.p, S, T, k, reinterpret_cast<int64_t*>(b_idx.p), st));
+    MW_TRY(mw_kpp_indices(big, S, T, k, d_idx, st));
     std::vector<int64_t> idx(k);
-    MW_HIP(hipMemcpyAsync(idx.data(), b_idx.p, k * 8, hipMemcpyDeviceToHost, st));
+    MW_HIP(hipMemcpyAsync(idx.data(), d_idx, k * 8, hipMemcpyDeviceToHost, st));
     MW_HIP(hipStreamSynchronize(st));
     idx[0] = first;
     MW_TRY(fit.scaled_rows(idx.data(), k, h_mu, h_inv, centers));
@@ -382,10 +460,9 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
       if (weight[j] == 0.0) empty.push_back(j);
     if (!empty.empty()) {
       const int ne = (int)empty.size();
-      if (!b_far.p) MW_TRY(dev_alloc<char>(b_far, mw_farthest_ws_bytes(S)));
       MW_HIP(hipMemcpyAsync(d_c64, centers.data(), centers.size() * 8, hipMemcpyHostToDevice, st));
       MW_TRY(mw_farthest(d_X, S, F, fit.a32, fit.b32, d_c64, k, d_labels, ne, d_topi, d_topv,
-                         b_far.p, st));
+                         big, st));
       std::vector<int64_t> far_i(ne);
       std::vector<double> far_v(ne);
       MW_HIP(hipMemcpyAsync(far_i.data(), d_topi, ne * 8, hipMemcpyDeviceToHost, st));
@@ -396,10 +473,12 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
       if (vmax != 0.0) {
         std::vector<double> xs;
         MW_TRY(fit.scaled_rows(far_i.data(), ne, h_mu, h_inv, xs));
+        std::vector<uint8_t> olds(ne);
+        for (int e = 0; e < ne; ++e)
+          MW_HIP(hipMemcpyAsync(&olds[e], d_labels + far_i[e], 1, hipMemcpyDeviceToHost, st));
+        MW_HIP(hipStreamSynchronize(st));
         for (int e = 0; e < ne; ++e) {
-          uint8_t old = 0;
-          MW_HIP(hipMemcpyAsync(&old, d_labels + far_i[e], 1, hipMemcpyDeviceToHost, st));
-          MW_HIP(hipStreamSynchronize(st));
+          const uint8_t old = olds[e];
           for (int f = 0; f < F; ++f) {
             cnew[(size_t)old * F + f] -= xs[(size_t)e * F + f];
             cnew[(size_t)empty[e] * F + f] = xs[(size_t)e * F + f];

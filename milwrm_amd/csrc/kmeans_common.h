@@ -105,6 +105,22 @@ __device__ __forceinline__ void dist4(f2v x, const f2v (&c)[4], f2v (&acc)[4]) {
         "+v"(acc[3])
       : "v"(x), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]));
 }
+// dist4 with the center pairs as scalar (SGPR) operands
+__device__ __forceinline__ void dist4_s(f2v x, const f2v (&c)[4], f2v (&acc)[4]) {
+  f2v d0, d1, d2, d3;
+  asm volatile(
+      "v_pk_add_f32 %0, %8, %9 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_add_f32 %1, %8, %10 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_add_f32 %2, %8, %11 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_add_f32 %3, %8, %12 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %4, %0, %0, %4\n\t"
+      "v_pk_fma_f32 %5, %1, %1, %5\n\t"
+      "v_pk_fma_f32 %6, %2, %2, %6\n\t"
+      "v_pk_fma_f32 %7, %3, %3, %7"
+      : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]),
+        "+v"(acc[3])
+      : "v"(x), "s"(c[0]), "s"(c[1]), "s"(c[2]), "s"(c[3]));
+}
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
 }
@@ -178,6 +194,61 @@ __device__ __forceinline__ void nearest_centers(const f2v (&x2)[FMAX / 2], const
         }
       }
     }
+  }
+}
+
+// nearest_centers with the pair-major image in global memory (gT, uniform
+// addresses): the center pairs arrive by scalar loads (s_load_dwordx8: one
+// feature pair of four centers) straight into the packed FMAs' SGPR operand,
+// so the E-step puts no traffic on the LDS pipe, which the CU's four SIMDs
+// share with the tile transposition (broadcast LDS reads of the centers made
+// the label pass LDS-bound).  Same fp32 operation sequence per center as
+// nearest_centers: bitwise the same distances.
+template <int FMAX, int KS, bool TOP2>
+__device__ __forceinline__ void nearest_centers_s(const f2v (&x2)[FMAX / 2],
+                                                  const f2v* __restrict__ gT, int k, int& lab,
+                                                  float& m1, float& m2) {
+  constexpr int NP = FMAX / 2;
+  lab = 0;
+  m1 = 0.f;
+  m2 = __builtin_inff();
+  for (int j0 = 0; j0 < k; j0 += 4) {
+    f2v acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f2v{0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const f2v* cp = gT + p * KS + j0;
+      const f2v c[4] = {cp[0], cp[1], cp[2], cp[3]};
+      dist4_s(x2[p], c, acc);  // pair order kept (asm): each pair's SGPRs die at once
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + q;
+      if (j < k) {
+        const float dd = acc[q].x + acc[q].y;
+        if (TOP2) {
+          if (j == 0) { m1 = dd; lab = 0; }
+          else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
+          else if (dd < m2) { m2 = dd; }
+        } else if (j == 0 || dd < m1) {
+          m1 = dd;
+          lab = j;
+        }
+      }
+    }
+  }
+}
+
+// pair-major image (FMAX/2 x KS float pairs) of k x F row-major centers in
+// global memory, for nearest_centers_s
+template <int FMAX, int KS>
+__global__ void __launch_bounds__(256) centers_T_kernel(const float* __restrict__ gc, int k, int F,
+                                                        f2v* __restrict__ gT) {
+  for (int q = threadIdx.x; q < (FMAX / 2) * KS; q += blockDim.x) {
+    const int p = q / KS, j = q - p * KS;
+    const int f0 = 2 * p, f1 = 2 * p + 1;
+    gT[q] = f2v{(j < k && f0 < F) ? gc[j * F + f0] : 0.f, (j < k && f1 < F) ? gc[j * F + f1] : 0.f};
   }
 }
 

@@ -364,7 +364,8 @@ __global__ void __launch_bounds__(256) mask_scatter_kernel(const uint8_t* __rest
 // Block b owns sample rows [b*R, (b+1)*R) in 256-row tiles.  Per tile: gather
 // rows into LDS, write them coalesced, and fold per-column Chan statistics.
 // Stats threads: f = t % F, part = t / F (nparts = 256 / F).  Record per block:
-// [n, mean[F], M2[F]].
+// [n, mean[F], M2[F], max|x|[F]] (the column maxima feed the fixed-point
+// exponents of the Lloyd M-step: no separate pass over the rows).
 __device__ __forceinline__ void chan_merge(double& n_a, double& m_a, double& q_a, double n_b,
                                            double m_b, double q_b) {
   if (n_b == 0.0) return;
@@ -395,6 +396,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   const bool st_on = t < nparts * F;
   const int sf = st_on ? t % F : 0, spart = st_on ? t / F : 0;
   double n_acc = 0.0, m_acc = 0.0, q_acc = 0.0;
+  float a_acc = 0.0f;
   // cooperative row loads: a wave instruction covers RPI rows x FP features
   const int FP = F <= 32 ? 32 : 64;
   const int RPI = 64 / FP;
@@ -432,7 +434,11 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
     // column statistics of this tile part
     if (st_on) {
       double s = 0.0, cnt = 0.0;
-      for (int r = spart; r < nrow; r += nparts) { s += (double)s_tile[r * F + sf]; cnt += 1.0; }
+      for (int r = spart; r < nrow; r += nparts) {
+        s += (double)s_tile[r * F + sf];
+        cnt += 1.0;
+        a_acc = fmaxf(a_acc, fabsf(s_tile[r * F + sf]));
+      }
       if (cnt > 0.0) {
         const double m = s / cnt;
         double q = 0.0;
@@ -448,21 +454,24 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   // merge parts in fixed order: stage (n, m, q) in LDS (reuse tile memory)
   double* s_st = reinterpret_cast<double*>(s_tile);
   if (st_on) {
-    s_st[3 * t + 0] = n_acc;
-    s_st[3 * t + 1] = m_acc;
-    s_st[3 * t + 2] = q_acc;
+    s_st[4 * t + 0] = n_acc;
+    s_st[4 * t + 1] = m_acc;
+    s_st[4 * t + 2] = q_acc;
+    s_st[4 * t + 3] = (double)a_acc;
   }
   __syncthreads();
-  double* out = rec + (size_t)blockIdx.x * (1 + 2 * F);
+  double* out = rec + (size_t)blockIdx.x * (1 + 3 * F);
   if (t < F) {
-    double n = 0.0, m = 0.0, q = 0.0;
+    double n = 0.0, m = 0.0, q = 0.0, a = 0.0;
     for (int part = 0; part < nparts; ++part) {
       const int u = part * F + t;
-      chan_merge(n, m, q, s_st[3 * u], s_st[3 * u + 1], s_st[3 * u + 2]);
+      chan_merge(n, m, q, s_st[4 * u], s_st[4 * u + 1], s_st[4 * u + 2]);
+      a = fmax(a, s_st[4 * u + 3]);
     }
     if (t == 0) out[0] = n;
     out[1 + t] = m;
     out[1 + F + t] = q;
+    out[1 + 2 * F + t] = a;
   }
 }
 
@@ -472,7 +481,7 @@ __global__ void __launch_bounds__(256) col_stats_kernel(const double* __restrict
                                                         double* __restrict__ st, int accumulate) {
   __shared__ double s_n[4][64], s_s[4][64], s_mean[64];
   const int f = threadIdx.x & 63, part = threadIdx.x >> 6;
-  const int rl = 1 + 2 * F;
+  const int rl = 1 + 3 * F;
   double n = 0.0, sm = 0.0, q = 0.0;
   double n0 = 0.0, m0 = 0.0, q0 = 0.0;
   if (accumulate && f < F) { n0 = st[0]; m0 = st[1 + f]; q0 = st[1 + F + f]; }
@@ -510,6 +519,25 @@ __global__ void __launch_bounds__(256) col_stats_kernel(const double* __restrict
     if (f == 0) st[0] = s_n[0][0];
     st[1 + f] = mean;
     st[1 + F + f] = Q;
+  }
+}
+
+// column max |x| over the block records (record field 1 + 2F + f), maxed
+// into out[f] when accumulating
+__global__ void __launch_bounds__(256) col_absmax_rec_kernel(const double* __restrict__ rec, int G, int F,
+                                                             float* __restrict__ out, int accumulate) {
+  __shared__ double s_a[4][64];
+  const int f = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int rl = 1 + 3 * F;
+  double a = 0.0;
+  if (f < F)
+    for (int b = part; b < G; b += 4) a = fmax(a, rec[(size_t)b * rl + 1 + 2 * F + f]);
+  s_a[part][f] = a;
+  __syncthreads();
+  if (part == 0 && f < F) {
+    for (int p2 = 1; p2 < 4; ++p2) a = fmax(a, s_a[p2][f]);
+    const float v = (float)a;  // a max of floats: exact
+    out[f] = accumulate ? fmaxf(out[f], v) : v;
   }
 }
 
@@ -693,7 +721,7 @@ int mw_mask_rank(const uint8_t* d_mask, int64_t n_pix, uint32_t* d_rank2pix, int
 }
 
 size_t mw_gather_ws_bytes(int64_t S, int F) {
-  return (size_t)stream_blocks(S) * (1 + 2 * (size_t)F) * sizeof(double) + 256;
+  return (size_t)stream_blocks(S) * (1 + 3 * (size_t)F) * sizeof(double) + 256;
 }
 
 int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F, const int32_t* d_idx,
@@ -705,7 +733,7 @@ int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F, cons
   const int G = stream_blocks(S);
   const int64_t R = rows_per_block(S);
   size_t lds = (size_t)kTile * F * sizeof(float);
-  if (lds < 3 * 256 * sizeof(double)) lds = 3 * 256 * sizeof(double);
+  if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
   hipLaunchKernelGGL(gather_kernel<true>, dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_idx,
                      d_rank2pix, S, R, d_X, reinterpret_cast<double*>(d_ws));
   MW_LAUNCH_CHECK();
@@ -717,7 +745,7 @@ int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stre
   MW_CHECK_ARG(S > 0 && F > 0 && F <= 64, "mw_col_stats_rows: bad shape S=%lld F=%d", (long long)S, F);
   hipStream_t st = as_stream(stream);
   size_t lds = (size_t)kTile * F * sizeof(float);
-  if (lds < 3 * 256 * sizeof(double)) lds = 3 * 256 * sizeof(double);
+  if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
   hipLaunchKernelGGL(gather_kernel<false>, dim3(stream_blocks(S)), dim3(256), lds, st, nullptr, F,
                      nullptr, F, nullptr, nullptr, S, rows_per_block(S), const_cast<float*>(d_X),
                      reinterpret_cast<double*>(d_ws));
@@ -847,6 +875,14 @@ int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats, i
   MW_CHECK_ARG(d_ws && d_stats && F > 0 && F <= 64, "mw_col_stats_finalize: bad args (F <= 64)");
   hipLaunchKernelGGL(col_stats_kernel, dim3(1), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), stream_blocks(S), F, d_stats, accumulate);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_col_stats_absmax(const void* d_ws, int64_t S, int F, float* d_out, int accumulate, void* stream) {
+  MW_CHECK_ARG(d_ws && d_out && S > 0 && F > 0 && F <= 64, "mw_col_stats_absmax: bad args (F <= 64)");
+  hipLaunchKernelGGL(col_absmax_rec_kernel, dim3(1), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const double*>(d_ws), stream_blocks(S), F, d_out, accumulate);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

@@ -270,9 +270,10 @@ def mask_rank(mask_u8: torch.Tensor, pending=None):
 
 
 def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2p: torch.Tensor,
-                X_out: torch.Tensor, stats: torch.Tensor, accumulate: bool):
+                X_out: torch.Tensor, stats: torch.Tensor, accumulate: bool, absmax=None):
     """X_out[j] = img[r2p[idx[j]], feat]; Chan-merge column stats into
-    ``stats`` = [n, mean[F], M2[F]] (fp64)."""
+    ``stats`` = [n, mean[F], M2[F]] (fp64); max |x| per column maxed into
+    ``absmax`` (fp32 [F], optional)."""
     H, W, C = img_f32.shape
     S, F = X_out.shape
     if S == 0:
@@ -282,9 +283,11 @@ def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2
         N.call("mw_gather_rows", P(img_f32), C, P(feat), F, P(idx), P(r2p), S, P(X_out), P(ws),
                stream())
     N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
+    if absmax is not None:
+        N.call("mw_col_stats_absmax", P(ws), S, F, P(absmax), 1, stream())
 
 
-def col_stats_rows(X: torch.Tensor, stats: torch.Tensor, accumulate: bool):
+def col_stats_rows(X: torch.Tensor, stats: torch.Tensor, accumulate: bool, absmax=None):
     """Column statistics of rows already in ``X`` (the records mw_gather_rows
     would produce for the same rows), Chan-merged into ``stats``."""
     S, F = X.shape
@@ -294,6 +297,8 @@ def col_stats_rows(X: torch.Tensor, stats: torch.Tensor, accumulate: bool):
     with profiling.timed("col_stats", S * F * 4):
         N.call("mw_col_stats_rows", P(X), S, F, P(ws), stream())
     N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
+    if absmax is not None:
+        N.call("mw_col_stats_absmax", P(ws), S, F, P(absmax), 1, stream())
 
 
 FUSED_USED = {"sample": 0, "assign": 0, "assign_banded": 0}  # deferred-blur paths taken (tests read it)

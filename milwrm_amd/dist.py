@@ -336,8 +336,9 @@ class DeviceKpp:
     def search(self, c, best, rv_local):
         D = self.D
         self.rv_dev.copy_(torch.from_numpy(rv_local))
-        self.N.call("mw_kpp_search", D.P(self.ws), self.rows.S, self.T, c, best, D.P(self.rv_dev),
-                    D.P(self.loc_dev), D.stream())
+        r = self.rows
+        self.N.call("mw_kpp_search", D.P(r.X), r.S, r.F, D.P(self.ws), self.T, c, best,
+                    D.P(self.rv_dev), D.P(self.loc_dev), D.stream())
         return self.loc_dev.cpu().numpy()
 
     def trial(self, c, best, cand_rows):

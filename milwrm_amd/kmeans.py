@@ -31,7 +31,7 @@ from .rng import as_random_state, first_center_index, kpp_draws
 class DeviceRows:
     """S x F fp32 rows in HBM, with x' = (x - mu) * inv applied on the fly."""
 
-    def __init__(self, X: torch.Tensor, mu=None, inv=None, feature_var=None):
+    def __init__(self, X: torch.Tensor, mu=None, inv=None, feature_var=None, xmax_local=None):
         assert X.dtype == torch.float32 and X.dim() == 2 and X.is_contiguous()
         self.X = X
         self.S, self.F = X.shape
@@ -46,6 +46,9 @@ class DeviceRows:
         self.b32 = D.h2d(self.b_host, dev)
         self._feature_var = feature_var
         self.xmax = None      # per-feature max |x| over all rows (all shards)
+        # max |x| of this shard's rows when the producer already took it
+        # (mw_col_stats_absmax beside the scaler statistics), else a pass
+        self._xmax_local = None if xmax_local is None else np.asarray(xmax_local, np.float32)
         self.qexp_dev = None  # fixed-point exponents of the Lloyd M-step (int32, device)
 
     def fixed_point(self, comm=None) -> np.ndarray:
@@ -54,7 +57,9 @@ class DeviceRows:
         a fixed-point sum back into a sum of x (lloyd.hip M-step)."""
         if self.qexp_dev is None:
             m = torch.empty(self.F, dtype=torch.float32, device=self.X.device)
-            if self.S:
+            if self._xmax_local is not None:
+                xmax = self._xmax_local.astype(np.float64)
+            elif self.S:
                 N.call("mw_col_absmax", D.P(self.X), self.S, self.F, D.P(m), D.stream())
                 xmax = D.d2h(m).astype(np.float64)
             else:
@@ -304,6 +309,9 @@ KIND_FIRST, KIND_TILE, KIND_QUEUE = 0, 1, 2
 # the k = 2..20 sweep at 10k^2 x 30 (tools/sweep_bench.py) took 1.05 / 1.03 /
 # 0.90 s at 0.03 / 0.06 / 0.12
 QUEUE_BELOW = float(os.environ.get("MW_LLOYD_QUEUE_BELOW", "0.12"))
+# KMeans.fit through the C++ driver (mw_kmeans_fit) where it applies; MW_KMEANS_C=0
+# keeps the Python loop (A/B and the per-pass trace)
+USE_C_FIT = os.environ.get("MW_KMEANS_C", "1") != "0"
 
 
 def _launch_pass(rows, fits_g, mode, kind, par, poff, outs, st, label="lloyd_pass"):
@@ -616,6 +624,11 @@ class KMeans:
                 rs_box.append(as_random_state(self.random_state))
             return rs_box[0]
 
+        seeded_int = isinstance(self.random_state, (int, np.integer)) \
+            and not isinstance(self.random_state, bool)
+        if (n_init == 1 and not comm.sharded() and not self.verbose and USE_C_FIT
+                and (arraylike or (init == "k-means++" and seeded_int))):
+            return self._set_fitted(rows, *self._fit_c(rows, k, init if arraylike else None))
         best = None
         for _ in range(n_init):
             if arraylike:
@@ -646,6 +659,39 @@ class KMeans:
             if best is None or inertia < best[1]:
                 best = (labels, inertia, centers, n_iter)
         return self._set_fitted(rows, *best)
+
+    def _fit_c(self, rows, k, init):
+        """The whole fit in the C++ driver (mw_kmeans_fit, csrc/fit.cpp): the
+        same control flow and fp64 host arithmetic as the Python path below
+        (bitwise the same result, tests/test_gpu_fit_c.py), without a Python
+        round trip per Lloyd iteration."""
+        S, F = rows.S, rows.F
+        mu = np.ascontiguousarray(rows.mu, dtype=np.float64)
+        inv = np.ascontiguousarray(rows.inv, dtype=np.float64)
+        var = np.ascontiguousarray(rows.feature_var(), dtype=np.float64) if self.tol else None
+        xmax = None if rows._xmax_local is None else np.ascontiguousarray(rows._xmax_local, np.float32)
+        c0 = None
+        if init is not None:
+            c0 = np.ascontiguousarray(np.array(init, dtype=np.float64))
+            if c0.shape != (k, F):
+                raise ValueError(f"The shape of the initial centers {c0.shape} does not "
+                                 f"match the number of clusters {k} / features {F}.")
+        labels = torch.empty(S, dtype=torch.uint8, device=rows.X.device)
+        centers = np.zeros((k, F))
+        inertia, n_iter = C.c_double(), C.c_int()
+        idx = np.full(k, -1, dtype=np.int64)
+        nb = N.query("mw_kmeans_fit_ws_bytes", S, F, k)
+        ws = D.WS.get("kfit", nb)
+        with profiling.timed("kmeans_fit", 0):
+            N.call("mw_kmeans_fit", D.P(rows.X), S, F, mu.ctypes.data, inv.ctypes.data,
+                   None if var is None else var.ctypes.data,
+                   None if xmax is None else xmax.ctypes.data, k,
+                   None if c0 is None else c0.ctypes.data, int(self.random_state or 0) & 0xFFFFFFFF,
+                   int(self.max_iter), float(self.tol or 0.0), D.P(labels), centers.ctypes.data,
+                   C.addressof(inertia), C.addressof(n_iter), idx.ctypes.data, D.P(ws), ws.numel(),
+                   D.stream())
+        self.init_indices_ = None if c0 is not None else idx
+        return labels, inertia.value, centers, n_iter.value
 
     def _kpp(self, rows, rs, comm):
         if comm.sharded():

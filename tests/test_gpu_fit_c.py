@@ -30,18 +30,23 @@ def _c_fit(X_dev, mu, inv, k, seed=18, var=None, init=None, max_iter=300, tol=1e
     n_iter = C.c_int()
     idx = np.full(k, -1, dtype=np.int64)
     N.call("mw_kmeans_fit", D.P(X_dev), S, F, mu.ctypes.data, inv.ctypes.data,
-           None if var is None else var.ctypes.data, k,
+           None if var is None else var.ctypes.data, None, k,
            None if init is None else init.ctypes.data, seed, max_iter, tol, D.P(labels),
            centers.ctypes.data, C.addressof(inertia), C.addressof(n_iter), idx.ctypes.data,
-           D.stream())
+           None, 0, D.stream())
     return dict(labels=labels.cpu().numpy().astype(np.int32), centers=centers,
                 inertia=inertia.value, n_iter=n_iter.value, idx=idx)
 
 
 def _py_fit(rows, k, seed=18, init="k-means++"):
-    from milwrm_amd.kmeans import KMeans
+    """The Python host loop (KMeans.fit with the C driver switched off)."""
+    from milwrm_amd import kmeans as K
 
-    km = KMeans(n_clusters=k, random_state=seed, init=init).fit(rows)
+    K.USE_C_FIT = False
+    try:
+        km = K.KMeans(n_clusters=k, random_state=seed, init=init).fit(rows)
+    finally:
+        K.USE_C_FIT = True
     return dict(labels=km.labels_, centers=km.cluster_centers_, inertia=km.inertia_,
                 n_iter=km.n_iter_, idx=km.init_indices_)
 

@@ -1,22 +1,17 @@
 #!/bin/bash
-# GPU pass (STEPS=tests,dist,bench,sweep,prof,pmc): parity tests, 2-rank sharded check, bench,
+# GPU pass (STEPS=tests,bench,sweep,prof,pmc): parity tests (incl. the 2-rank sharded test), bench,
 # k-sweep bench, rocprofv3 kernel stats, PMC HBM traffic passes; each step under its own limit.
 #   gpurun -- bash tools/gpu/round_pass.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 R="$GRAFT_REPO_ROOT"
-STEPS="${STEPS:-tests,dist,bench,sweep,prof,pmc}"
+STEPS="${STEPS:-tests,bench,sweep,prof,pmc}"
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 if has tests; then
   echo "[gpu] pytest -m gpu"
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/pytest_gpu.log | head; exit $rc; }
-fi
-if has dist; then
-  echo "[gpu] sharded check (2 ranks, one GPU)"
-  timeout -k 10 300 torchrun --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 tests/dist_gpu_check.py > gpurun_out/dist_check.log 2>&1
-  rc=$?; grep -E "dist_gpu_check|Error|error" gpurun_out/dist_check.log | tail -5; [ $rc -eq 0 ] || { echo "dist rc=$rc"; exit $rc; }
 fi
 if has bench; then
   echo "[gpu] bench"

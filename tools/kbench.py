@@ -111,24 +111,26 @@ def main():
         idxo = torch.empty(k, dtype=torch.int64, device="cuda")
         N.call("mw_kpp_indices", D.P(ws), S, T, k, D.P(idxo), st)
         res["kpp(init+7 steps)"] = (ms, k * (S * F * 4) + (k - 1) * S * 8 * (1 + T), fp(idxo))
+    if want("lloyd"):
+        # the real Lloyd sequence (first / tile / queue passes, final mode 1)
+        # from evenly spaced rows, per-launch HIP event times (kmeans.TRACE)
+        from milwrm_amd import kmeans as K
+
+        rows = K.DeviceRows(X, mu64.cpu().numpy(), inv64.cpu().numpy())
+        c0 = rows.scaled_rows(np.arange(0, S, S // k)[:k])
+        K.lloyd_device(rows, c0)  # warm (fixed point, workspaces)
+        K.TRACE = []
+        labels, inertia, cents, n_iter = K.lloyd_device(rows, c0)
+        per = {}
+        for t in K.trace_summary():
+            per.setdefault((t["mode"], t["kind"]), []).append(t["ms"])
+        K.TRACE = None
+        for (mode, kind), v in sorted(per.items()):
+            res[f"lloyd_m{mode}_{kind or 'full'} x{len(v)}"] = (float(np.mean(v)), S * (F * 4 + 9),
+                                                                fp(labels))
+        print(f"lloyd n_iter {n_iter} inertia {inertia!r}", flush=True)
     cent = X[torch.arange(0, S, S // k, device="cuda")[:k]].double()
     cent = ((cent - mu64) * inv64).float().contiguous()
-    labels = torch.full((S,), 255, dtype=torch.uint8, device="cuda")
-    lws = D.WS.get("lloyd", N.query("mw_lloyd_ws_bytes", S, k, F))
-    out = torch.empty(k * F + k + 2, dtype=torch.float64, device="cuda")
-    for mode in (0, 1):
-        if not want(f"lloyd{mode}") and not want("lloyd"):
-            continue
-
-        def ll():
-            N.call("mw_lloyd_step", D.P(X), S, F, D.P(a32), D.P(b32), D.P(cent), k, D.P(labels),
-                   mode, D.P(lws), st)
-        labels.fill_(255)
-        ms = timeit(ll, a.reps)
-        labels.fill_(255)
-        ll()
-        N.call("mw_lloyd_reduce", D.P(lws), S, k, F, D.P(out), st)
-        res[f"lloyd_mode{mode}"] = (ms, S * (F * 4 + 2), fp(labels, out))
     if want("assign"):
         lab = torch.empty((H, W), dtype=torch.int8, device="cuda")
         conf = torch.empty((H, W), dtype=torch.float32, device="cuda")
