@@ -78,6 +78,16 @@ __device__ __forceinline__ float lognorm1(float x, float inv, float p) {
   return l2 * 0.30102999566398120f - (e * rcp_coarse(v)) * 0.43429448190325182f;
 }
 
+// log2(t + p) on an element pair, no rounding correction: the matrix-core
+// kernel folds log10(2) into its horizontal taps.  The rounding of t + p moves
+// the result by <= 2^-24 / ln 2 absolute (2.6e-8 after the log10 scale) —
+// far inside the fp32 blur's own rounding for values of order 1, and 2
+// instructions per pair instead of 9 on a VALU-issue-bound kernel.
+__device__ __forceinline__ bf2 log2norm2(bf2 x, bf2 inv, float p) {
+  const bf2 v = __builtin_elementwise_fma(x, inv, bf2{p, p});
+  return bf2{__builtin_amdgcn_logf(v.x), __builtin_amdgcn_logf(v.y)};
+}
+
 // the same on an element pair with packed arithmetic (v_pk_*; the two
 // transcendentals per element stay scalar)
 __device__ __forceinline__ bf2 lognorm2(bf2 x, bf2 inv, float p) {

@@ -263,10 +263,11 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
   // input column of the tile's halo'd span), B = LDS row reads
   const int m = lane & 15, kq = lane >> 4;
   float a_op[NK];
+  const float tap_scale = LOGN ? 0.30102999566398120f : 1.f;  // log2 -> log10 (log2norm2)
 #pragma unroll
   for (int st = 0; st < NK; ++st) {
     const int j = 4 * st + kq - m;
-    a_op[st] = (j >= 0 && j <= 2 * R) ? taps.w[j] : 0.f;
+    a_op[st] = (j >= 0 && j <= 2 * R) ? taps.w[j] * tap_scale : 0.f;
   }
   // B[k][n] for k-step st: column 16*tx + 4*st + kq, channel 16*ct + n (n = m)
   const int b_ct = SWZ ? (ct ^ (kq & 1)) : ct;  // (16*tx + 4*st + kq) & 1 == kq & 1
@@ -352,7 +353,7 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
       for (int i = 0; i < CP; ++i) {
         bf2 x = Chunk16<T>::pair(v, i);
 #ifndef MW_X_NOLOG
-        if (LOGN) x = lognorm2(x, p_inv[c * CP + i], pseudo);
+        if (LOGN) x = log2norm2(x, p_inv[c * CP + i], pseudo);  // log10(2): in the taps
 #endif
         const int d = p_dst[c * CP + i];
         *reinterpret_cast<bf2*>(d >= 0 ? dst + d : s_dummy) = x;  // pad pairs: the sink

@@ -14,7 +14,7 @@ size = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 torch.cuda.set_device(0)
 raw, mask = D.synth_slide(size, size, C, seed=7, mode="hard")
-inv = torch.rand(C, device="cuda", dtype=torch.float32) * 1e-3 + 1e-4
+inv = ((torch.arange(C, device="cuda", dtype=torch.float32) * 37) % 11 + 1) * 1e-4  # deterministic
 ref = None
 variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["", "MW_BLUR_BH=256"]
 for bw in variants:
@@ -37,5 +37,8 @@ for bw in variants:
     same = None if ref is None else bool(torch.equal(out, ref))
     if ref is None:
         ref = out.clone()
+        if os.environ.get("BLUR_SAVE"):  # strided sample of the first variant, for cross-library checks
+            import numpy as np
+            np.save(os.environ["BLUR_SAVE"], out.view(size, size, C)[::37, ::41].cpu().numpy())
     print(f"BW={bw or 'default'}: {ms:.3f} ms/launch, {gb / ms * 1e3:.0f} GB/s algorithmic, same={same}",
           flush=True)
