@@ -230,6 +230,10 @@ def _assign_img(image: img, features, centers, scaler):
         if res is not None:
             return res
     src = D.as_float32(image._materialize())
+    band = getattr(image, "_band", None)
+    if band is not None:  # label the band rows only (milwrm_amd.bands)
+        return assign_image(src[band.rows], feats, mu, inv, centers,
+                            D.padded_mask(image._mask_device()[band.rows].contiguous()))
     return assign_image(src, feats, mu, inv, centers, image._mask_device())
 
 
@@ -405,7 +409,13 @@ class mxif_labeler(tissue_labeler):
         # boolean selection (one pass instead of a selection per batch)
         per = {}
         df = self.image_df
-        for batch, est, px in zip(df["batch_names"], df["mean estimators"], df["pixels"]):
+        for im, batch, est, px in zip(df["Img"], df["batch_names"], df["mean estimators"],
+                                      df["pixels"]):
+            band = getattr(im, "_band", None)
+            if band is not None and band.band != 0:
+                # a slide split into row bands (milwrm_amd.bands): every band
+                # reports the whole slide's estimators; count them once
+                est, px = np.zeros(len(est)), 0
             acc = per.setdefault(batch, [0, 0])
             acc[0] = acc[0] + np.array(est)
             acc[1] = acc[1] + px
@@ -439,6 +449,21 @@ class mxif_labeler(tissue_labeler):
                 images.append(img.from_npz(image + ".npz"))
             else:
                 images.append(image)
+        if getattr(images[0], "_band", None) is not None:
+            # one slide in row bands over the ranks (milwrm_amd.bands)
+            from .bands import prep_banded
+
+            X, img_stats, xmax = prep_banded(images[0], self.image_df["batch_names"].iloc[0],
+                                             means, features, filter_name, sigma, fract, comm)
+            self._batch_counts = [int(X.shape[0])]
+            self._images = images
+            st = comm.merge_image_stats(D.d2h(img_stats), X.shape[1])
+            self.scaler = StandardScaler.from_stats(st)
+            mu, inv = self.scaler.affine()
+            self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv,
+                                    xmax_local=D.d2h(xmax))
+            self._cluster_host = None
+            return
         # phase 1: mask ranks → sample counts → one preallocated row block
         dev = D.device()
         ranks = [im._mask_rank() for im in images]
@@ -520,7 +545,7 @@ class mxif_labeler(tissue_labeler):
         the label pass's per-domain pixel counts; then the stacked bar plot."""
         k = int(self.k)
         if getattr(self, "_dom_dev", None):
-            doms = D.d2h(torch.stack(self._dom_dev))
+            doms = self._slide_doms()
             counts = doms[:, k:2 * k].T  # domains x images
         else:
             counts = np.array([[np.sum(np.asarray(t) == j) for t in self.tissue_IDs]
@@ -539,13 +564,22 @@ class mxif_labeler(tissue_labeler):
         self.tissue_ID_proportion = df_count
         return _stacked_bar(df_count.T, cmap, figsize, "images", save_to)
 
+    def _slide_doms(self) -> np.ndarray:
+        """images x [per-domain confidence sums | pixel counts] from the label
+        pass; a slide split into row bands (milwrm_amd.bands) sums its bands."""
+        t = torch.stack(self._dom_dev)
+        ims = getattr(self, "_images", None) or []
+        if ims and getattr(ims[0], "_band", None) is not None and self._comm.sharded():
+            t = self._comm.all_reduce_(t.clone())
+        return D.d2h(t)
+
     def confidence_score_images(self):
         """MILWRM.py:1868-1900 from the fused pass: confidence_IDs and the
         images x domains DataFrame of mean confidences."""
         k = self.kmeans.cluster_centers_.shape[0]
         # images x domains, the frame the reference concatenates row by row
         # (index 0..n-1, columns 0..k-1), built in one constructor call
-        doms = D.d2h(torch.stack(self._dom_dev)) if self._dom_dev else np.zeros((0, 2 * k))
+        doms = self._slide_doms() if self._dom_dev else np.zeros((0, 2 * k))
         rows = [list(domain_means(dom, k).values()) for dom in doms]
         self.confidence_IDs = _LazyHostList(list(self._conf_dev), _conf_to_host)
         self.confidence_score_df = pd.DataFrame(np.asarray(rows, dtype=np.float64).reshape(-1, k))

@@ -77,6 +77,7 @@ class img:
                 "Shape of mask must match the first two dimensions of img_arr"
         self.mask = mask
         self._mask_dev = None
+        self._band = None  # bands.BandInfo when this img is one row band of a slide
 
     # ----------------------------------------------------------- residency
     @property
@@ -240,6 +241,7 @@ class img:
         obj._mask = None
         obj._mask_dev = None
         obj._mrank = None
+        obj._band = None
         if mask is not None:
             obj._mask = _DeviceMask(mask)
             obj._mask_dev = (mask != 0).to(torch.uint8) if mask.dtype != torch.uint8 else mask
@@ -395,9 +397,21 @@ class img:
         out = D.block_mean(self._materialize(), int(fact))
         self._set_device(out)
 
-    def calculate_non_zero_mean(self):
+    def calculate_non_zero_mean(self, comm=None):
         """MxIF.py:519-541: ([mean_c * pixels], pixels) with pixels = non-zero
-        elements over all channels."""
+        elements over all channels.  A row band of a slide (milwrm_amd.bands)
+        sums its band rows and all-reduces the exact integer-valued sums over
+        ``comm``: every band returns the whole slide's values."""
+        if getattr(self, "_band", None) is not None:
+            s, c = D.nz_stats(self._materialize()[self._band.rows].contiguous())
+            if comm is not None and comm.sharded():
+                comm.all_reduce_(s)
+                comm.all_reduce_(c)
+            s, c = D.d2h(s, c)
+            pixels = int(c.sum())
+            with np.errstate(invalid="ignore", divide="ignore"):
+                means = s / c
+            return [float(m) * pixels for m in means], pixels
         s, c = D.nz_stats(self._materialize())
         self._prefetch_mask_rank()  # queued behind nz_stats, overlaps the host work that follows
         s, c = D.d2h(s, c)

@@ -108,6 +108,16 @@ class DistComm(LocalComm):
             dist.all_reduce(t, group=self.group)
         return t
 
+    def all_to_all_counts(self, counts):
+        """counts[d] sent to rank d -> counts received from each rank."""
+        t = torch.as_tensor(np.asarray(counts, dtype=np.int64), device=self.device)
+        out = torch.empty_like(t)
+        dist.all_to_all_single(out, t, group=self.group)
+        return out.cpu().tolist()
+
+    def all_to_all_single(self, out, src, out_splits, in_splits):
+        dist.all_to_all_single(out, src, out_splits, in_splits, group=self.group)
+
     def all_reduce_max_np(self, a: np.ndarray) -> np.ndarray:
         t = torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=self.device).clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)

@@ -213,3 +213,77 @@ def test_gloo_world2_kpp_and_farthest_merge():
         np.testing.assert_allclose(val, d[want], rtol=1e-12)
         np.testing.assert_allclose(xs, Xs[want], rtol=1e-12)
         np.testing.assert_array_equal(old, lab[want])
+
+
+def _band_worker(rank, world, port, q):
+    """milwrm_amd.bands routing over gloo: the rows of the draws in this band
+    travel to the rank owning their draw position, arriving in draw order."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from milwrm_amd import bands
+        from milwrm_amd.dist import DistComm
+
+        comm = DistComm(device=torch.device("cpu"))
+        Ms = np.array([1000, 0, 2517][:world] if world == 3 else [1000, 2517])
+        off = np.concatenate([[0], np.cumsum(Ms)])
+        M = int(off[-1])
+        idx = np.random.RandomState(16).randint(M, size=M // 5)  # the reference's draws
+        S = idx.size
+        bnd = bands.owner_bounds(S, world)
+        idx64 = torch.as_tensor(idx, dtype=torch.int64)
+        pos, local_idx, send = bands.route_draws(idx64, off, rank, bnd)
+        # a "row" = (global mask rank, draw position, 7)
+        rows = torch.stack([(local_idx.to(torch.float64) + off[rank]), pos.to(torch.float64),
+                            torch.full((pos.numel(),), 7.0, dtype=torch.float64)], 1)
+        recv, counts = bands.exchange_rows(rows, send, comm)
+        X = bands.assemble_rows(recv, idx64, off, bnd, rank)
+        q.put((rank, X.numpy(), counts, bnd))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.timeout(120)
+def test_gloo_row_band_exchange(world):
+    """One slide in row bands (milwrm_amd.bands): after the
+    all-to-all every rank holds exactly the rows of its contiguous range of
+    draw positions, in draw order — the layout the sharded fit expects.  The
+    3-rank case has an empty band (no masked pixels)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_band_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in [q.get(timeout=90) for _ in ps])
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    Ms = [1000, 0, 2517] if world == 3 else [1000, 2517]
+    M = sum(Ms)
+    idx = np.random.RandomState(16).randint(M, size=M // 5)
+    for r in range(world):
+        X, counts, bnd = res[r]
+        j = np.arange(bnd[r], bnd[r + 1])
+        np.testing.assert_array_equal(X[:, 0], idx[j])
+        np.testing.assert_array_equal(X[:, 1], j)
+        assert (X[:, 2] == 7).all()
+        assert sum(counts) == j.size
+
+
+def test_band_rows_cover_slide():
+    from milwrm_amd.bands import band_rows
+
+    for H, n in [(10, 1), (10, 3), (97, 4), (8, 8)]:
+        prev = 0
+        for b in range(n):
+            y0, y1, lo, hi = band_rows(H, n, b, halo=8)
+            assert y0 == prev and y1 > y0 and lo == max(0, y0 - 8) and hi == min(H, y1 + 8)
+            prev = y1
+        assert prev == H
+    with pytest.raises(ValueError):
+        band_rows(4, 5, 0)

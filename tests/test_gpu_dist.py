@@ -106,3 +106,98 @@ def test_two_shards_bitwise_equal_single_process(gpu):
     # clustering rows: rank order = image order
     np.testing.assert_array_equal(np.concatenate([got[0]["rows_labels"], got[1]["rows_labels"]]),
                                   ref["rows_labels"])
+
+
+def _band_worker(rank, world, port, q):
+    """One slide in row bands (milwrm_amd.bands): rank b preprocesses rows
+    [y0, y1) (+ 8 halo rows), the sampled rows move by one all-to-all to
+    the rank owning their draw positions, the fit runs row-sharded."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        import milwrm_amd as M
+        from milwrm_amd import bands
+        from milwrm_amd.dist import DistComm
+
+        comm = DistComm(device=torch.device("cpu"))
+        raw, mask = _band_slide()
+        im = bands.band_image(raw, mask, rank, world, halo=8)
+        est, pix = im.calculate_non_zero_mean(comm)
+        df = pd.DataFrame({"Img": [im], "batch_names": ["b1"], "mean estimators": [est],
+                           "pixels": [pix]})
+        lab = M.mxif_labeler(df)
+        lab.prep_cluster_data(features=list(range(8)), sigma=2, fract=0.2, comm=comm)
+        lab.label_tissue_regions(k=6, plot_out=False, random_state=18, comm=comm)
+        lab.confidence_score_images()
+        out = dict(est=np.asarray(est), pix=pix, mean=lab.scaler.mean_, scale=lab.scaler.scale_,
+                   idx=lab.kmeans.init_indices_, n_iter=lab.kmeans.n_iter_,
+                   centers=lab.kmeans.cluster_centers_, inertia=lab.kmeans.inertia_,
+                   rows_labels=lab.kmeans.labels_, tid=np.nan_to_num(lab.tissue_IDs[0], nan=-1),
+                   cid=np.nan_to_num(lab.confidence_IDs[0], nan=-1),
+                   conf_df=lab.confidence_score_df.values, rows=(im._band.y0, im._band.y1))
+        torch.cuda.synchronize()
+        q.put((rank, out))
+    except Exception as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _band_slide():
+    from oracle.milwrm_oracle import synth_slide
+
+    return synth_slide(208, 176, 8, seed=411, mode="hard")
+
+
+@pytest.mark.timeout(600)
+def test_row_bands_equal_single_process(gpu):
+    """a single slide split into 2 row bands over 2 ranks gives
+    the single-process result: the same estimators, k-means++ indices,
+    n_iter, every pixel's label; centers / inertia / confidences to fp64
+    rounding (the scaler statistics of the two row ranges are Chan-merged)."""
+    import milwrm_amd as M
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_band_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=540) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for r in (0, 1):
+        assert not isinstance(got[r], str), got[r]
+        assert ps[r].exitcode == 0
+    raw, mask = _band_slide()
+    im = M.img(raw.copy(), mask=mask.copy())
+    est, pix = im.calculate_non_zero_mean()
+    df = pd.DataFrame({"Img": [im], "batch_names": ["b1"], "mean estimators": [est],
+                       "pixels": [pix]})
+    lab = M.mxif_labeler(df)
+    lab.prep_cluster_data(features=list(range(8)), sigma=2, fract=0.2)
+    lab.label_tissue_regions(k=6, plot_out=False, random_state=18)
+    lab.confidence_score_images()
+    tid = np.nan_to_num(lab.tissue_IDs[0], nan=-1)
+    cid = np.nan_to_num(lab.confidence_IDs[0], nan=-1)
+    for r in (0, 1):
+        g = got[r]
+        np.testing.assert_array_equal(g["est"], np.asarray(est))
+        assert g["pix"] == pix
+        np.testing.assert_allclose(g["mean"], lab.scaler.mean_, rtol=1e-13)
+        np.testing.assert_allclose(g["scale"], lab.scaler.scale_, rtol=1e-13)
+        np.testing.assert_array_equal(g["idx"], lab.kmeans.init_indices_)
+        assert g["n_iter"] == lab.kmeans.n_iter_
+        np.testing.assert_allclose(g["centers"], lab.kmeans.cluster_centers_, rtol=1e-10, atol=1e-12)
+        assert abs(g["inertia"] - lab.kmeans.inertia_) <= 1e-10 * abs(lab.kmeans.inertia_)
+        y0, y1 = g["rows"]
+        np.testing.assert_array_equal(g["tid"], tid[y0:y1])
+        np.testing.assert_allclose(g["cid"], cid[y0:y1], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(g["conf_df"], lab.confidence_score_df.values, rtol=1e-10)
+    np.testing.assert_array_equal(np.concatenate([got[0]["rows_labels"], got[1]["rows_labels"]]),
+                                  lab.kmeans.labels_)
