@@ -123,25 +123,106 @@ __global__ void __launch_bounds__(256) nz_stats_kernel(const T* __restrict__ img
   }
 }
 
-__global__ void nz_stats_reduce(const double* __restrict__ part, int G, int C,
-                                double* __restrict__ sum, int64_t* __restrict__ cnt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s[4] = {0, 0, 0, 0}, n[4] = {0, 0, 0, 0};
-  int b = 0;
-  for (; b + 3 < G; b += 4) {
+// uint16 slides (the MxIF case): exact integer accumulation, two VALU
+// operations per element instead of a fp64 add, an int64 add and conversions
+// (the fp64 form made this pure read stream VALU-bound at 4.4 TB/s).  Per
+// lane and 16-byte load (8 channels, 4 words of 2): the low and high halves
+// of each word go into uint32 sums, and min(word, 0x00010001) -- 1 per
+// non-zero half -- into packed uint16 counts (v_pk_min_u16 / v_pk_add_u16).
+// The 32-bit sums and 16-bit counts are flushed to 64-bit totals every
+// kNzFlush loads (65535 * kNzFlush < 2^32, kNzFlush < 2^16).  Block records
+// as nz_stats_kernel: [C sums | C counts], integer-valued fp64.
+typedef unsigned short nz_us2 __attribute__((ext_vector_type(2)));
+constexpr int kNzFlush = 32768;
+__global__ void __launch_bounds__(256) nz_stats_u16_kernel(const uint16_t* __restrict__ img,
+                                                           int64_t n_elem, int C, int teff,
+                                                           int64_t epb, double* __restrict__ part) {
+  constexpr int V = 8;
+  __shared__ unsigned long long s_sum[256 * V];
+  __shared__ unsigned int s_cnt[256 * V];
+  const int t = threadIdx.x;
+  const int64_t lo = (int64_t)blockIdx.x * epb;
+  const int64_t hi = min(n_elem, lo + epb);
+  unsigned long long tot[V], totc[V];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      s[u] += part[(size_t)(b + u) * 2 * C + c];
-      n[u] += part[(size_t)(b + u) * 2 * C + C + c];
+  for (int i = 0; i < V; ++i) { tot[i] = 0ull; totc[i] = 0ull; }
+  if (t < teff) {
+    const int64_t stride = (int64_t)teff * V;
+    int64_t e = lo + (int64_t)t * V;
+    while (e < hi) {
+      unsigned int sum[V];
+      nz_us2 cnt[V / 2];
+#pragma unroll
+      for (int i = 0; i < V; ++i) sum[i] = 0u;
+#pragma unroll
+      for (int j = 0; j < V / 2; ++j) cnt[j] = nz_us2{0, 0};
+      auto take = [&](const uint4& w4) {
+        const unsigned int w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sum[2 * j] += w[j] & 0xffffu;
+          sum[2 * j + 1] += w[j] >> 16;
+          const nz_us2 h = __builtin_bit_cast(nz_us2, w[j]);
+          cnt[j] += __builtin_elementwise_min(h, nz_us2{1, 1});
+        }
+      };
+      // up to kNzFlush loads, four 16-B loads in flight
+      int n = 0;
+      for (; n + 4 <= kNzFlush && e + 3 * stride + V <= hi; n += 4, e += 4 * stride) {
+        uint4 w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const uint4*>(img + e + u * stride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) take(w[u]);
+      }
+      for (; n < kNzFlush && e + V <= hi; ++n, e += stride) take(*reinterpret_cast<const uint4*>(img + e));
+      if (n < kNzFlush && e < hi) {  // tail (partial vector): same lane, same channels
+        uint4 w4 = uint4{0u, 0u, 0u, 0u};
+        unsigned int* wp = reinterpret_cast<unsigned int*>(&w4);
+        for (int i = 0; i < V; ++i)
+          if (e + i < hi) wp[i >> 1] |= (unsigned int)img[e + i] << (16 * (i & 1));
+        take(w4);
+        e = hi;
+      }
+#pragma unroll
+      for (int j = 0; j < V / 2; ++j) {
+        tot[2 * j] += sum[2 * j];
+        tot[2 * j + 1] += sum[2 * j + 1];
+        totc[2 * j] += cnt[j].x;
+        totc[2 * j + 1] += cnt[j].y;
+      }
     }
   }
-  for (; b < G; ++b) {
-    s[0] += part[(size_t)b * 2 * C + c];
-    n[0] += part[(size_t)b * 2 * C + C + c];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { s_sum[t * V + i] = tot[i]; s_cnt[t * V + i] = (unsigned int)totc[i]; }
+  __syncthreads();
+  if (t < C) {
+    unsigned long long sm = 0ull, nn = 0ull;
+    for (int q = t; q < teff * V; q += C) { sm += s_sum[q]; nn += s_cnt[q]; }
+    part[(size_t)blockIdx.x * 2 * C + t] = (double)sm;
+    part[(size_t)blockIdx.x * 2 * C + C + t] = (double)nn;
   }
-  sum[c] = (s[0] + s[1]) + (s[2] + s[3]);
-  cnt[c] = (int64_t)((n[0] + n[1]) + (n[2] + n[3]));
+}
+
+// per channel (one workgroup each) the sum of the G block records: integer-
+// valued fp64 below 2^53, so exact in any order
+__global__ void __launch_bounds__(256) nz_stats_reduce(const double* __restrict__ part, int G, int C,
+                                                       double* __restrict__ sum, int64_t* __restrict__ cnt) {
+  __shared__ double s_s[256], s_n[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  double sm = 0.0, n = 0.0;
+  for (int b = t; b < G; b += 256) {
+    sm += part[(size_t)b * 2 * C + c];
+    n += part[(size_t)b * 2 * C + C + c];
+  }
+  s_s[t] = sm;
+  s_n[t] = n;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) { s_s[t] += s_s[t + o]; s_n[t] += s_n[t + o]; }
+    __syncthreads();
+  }
+  if (t == 0) { sum[c] = s_s[0]; cnt[c] = (int64_t)s_n[0]; }
 }
 
 static inline int gcd_i(int a, int b) { while (b) { int t = a % b; a = b; b = t; } return a; }
@@ -325,20 +406,30 @@ __global__ void __launch_bounds__(1024) mask_scan_kernel(uint32_t* __restrict__ 
 __global__ void __launch_bounds__(256) mask_scatter_kernel(const uint8_t* __restrict__ m, int64_t n,
                                                            const uint32_t* __restrict__ base,
                                                            uint32_t* __restrict__ r2p) {
+  // per 4096-pixel step: 16 mask bytes per lane in one 16-byte load, a block
+  // scan of the per-lane counts, the step's pixel indices staged in LDS at
+  // their ranks, then written as one contiguous coalesced run
   __shared__ uint32_t s_w[4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __shared__ uint32_t s_pix[4096];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   uint32_t run = base[blockIdx.x];
   const int64_t lo = (int64_t)blockIdx.x * kMaskChunk;
   for (int it = 0; it < kMaskChunk / 4096; ++it) {
-    const int64_t p = lo + (int64_t)it * 4096 + threadIdx.x * 16;
+    const int64_t p = lo + (int64_t)it * 4096 + t * 16;
     uint32_t bits = 0;  // 16 flags
-    for (int q = 0; q < 16; ++q) {
-      const int64_t pp = p + q;
-      if (pp < n && m[pp]) bits |= 1u << q;
+    if (p + 16 <= n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(m + p);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bits |= ((w[k] >> (8 * q)) & 0xFFu) ? 1u << (4 * k + q) : 0u;
+    } else {
+      for (int q = 0; q < 16; ++q)
+        if (p + q < n && m[p + q]) bits |= 1u << q;
     }
     const uint32_t c = __popc(bits);
-    // inclusive scan within the wave
-    uint32_t incl = c;
+    uint32_t incl = c;  // inclusive scan within the wave
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t v = __shfl_up(incl, o, 64);
@@ -348,15 +439,17 @@ __global__ void __launch_bounds__(256) mask_scatter_kernel(const uint8_t* __rest
     __syncthreads();
     uint32_t wbase = 0;
     for (int w = 0; w < wid; ++w) wbase += s_w[w];
-    uint32_t pos = run + wbase + incl - c;
+    uint32_t loc = wbase + incl - c;
     while (bits) {
       const int q = __ffs(bits) - 1;
       bits &= bits - 1;
-      r2p[pos++] = (uint32_t)(p + q);
+      s_pix[loc++] = (uint32_t)(p + q);
     }
     const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
     __syncthreads();
+    for (uint32_t i = t; i < tot; i += 256) r2p[run + i] = s_pix[i];
     run += tot;
+    __syncthreads();  // s_pix / s_w reused by the next step
   }
 }
 
@@ -389,7 +482,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
                                                      double* __restrict__ rec) {
   extern __shared__ __attribute__((aligned(16))) float s_tile[];  // 256*F floats + stats scratch
   __shared__ int s_feat[64];
-  __shared__ uint32_t s_pix[256];
+  __shared__ uint32_t s_pix[2][256];  // pixel of each row of this tile / the next one
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   for (int f = t; f < 64; f += 256) s_feat[f] = (GATHER && f < F) ? feat[f] : 0;
   const int nparts = 256 / F;
@@ -405,18 +498,31 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   const int64_t hi = min(S, lo + R);
   __syncthreads();
   const int fcol = lf < F ? (GATHER ? s_feat[lf] : lf) : 0;
-  for (int64_t r0 = lo; r0 < hi; r0 += kTile) {
+  // the sample -> pixel lookups (idx, then r2p: two dependent random reads)
+  // of tile i+1 are issued before tile i's row loads and stored after them
+  if (GATHER && lo < hi && t < (int)min((int64_t)kTile, hi - lo)) s_pix[0][t] = r2p[idx[lo + t]];
+  int buf = 0;
+  for (int64_t r0 = lo; r0 < hi; r0 += kTile, buf ^= 1) {
     const int nrow = (int)min((int64_t)kTile, hi - r0);
-    if (GATHER && t < nrow) s_pix[t] = r2p[idx[r0 + t]];
     __syncthreads();
+    const uint32_t* pix = s_pix[buf];
+    const int64_t r1 = r0 + kTile;
+    const bool nxt = GATHER && r1 < hi && t < (int)min((int64_t)kTile, hi - r1);
+    const int32_t nidx = nxt ? idx[r1 + t] : 0;
     // wave wid loads rows [wid*64, wid*64+64) of the tile, RPI rows per instruction
     constexpr int kBatch = 16;
+    uint32_t npix = 0;
+    bool npix_issued = false;
     for (int i0 = 0; i0 < 64 / RPI; i0 += kBatch) {
+      if (i0 == kBatch && nxt) {  // nidx has landed with the first batch of rows
+        npix = r2p[nidx];
+        npix_issued = true;
+      }
       float v[kBatch];
 #pragma unroll
       for (int i = 0; i < kBatch; ++i) {
         const int row = min(wid * 64 + (i0 + i) * RPI + lr, nrow - 1);  // clamped: always valid
-        v[i] = GATHER ? img[(int64_t)s_pix[row] * C + fcol] : X[(r0 + row) * F + fcol];
+        v[i] = GATHER ? img[(int64_t)pix[row] * C + fcol] : X[(r0 + row) * F + fcol];
       }
 #pragma unroll
       for (int i = 0; i < kBatch; ++i) {
@@ -424,6 +530,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
         if (i0 + i < 64 / RPI && row < nrow && lf < F) s_tile[row * F + lf] = v[i];
       }
     }
+    if (nxt) s_pix[buf ^ 1][t] = npix_issued ? npix : r2p[nidx];
     __syncthreads();
     // coalesced write of the tile (rows contiguous in X)
     if (GATHER) {
@@ -477,16 +584,22 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
 
 // Merge per-block (n, mean, M2) records: n = sum n_b, mean = sum n_b m_b / n,
 // M2 = sum [M2_b + n_b (m_b - mean)^2]  (fixed order; optional prior record).
-__global__ void __launch_bounds__(256) col_stats_kernel(const double* __restrict__ rec, int G, int F,
-                                                        double* __restrict__ st, int accumulate) {
-  __shared__ double s_n[4][64], s_s[4][64], s_mean[64];
+// Fixed-order fold of the G per-block Chan records: 16 parts x 64 features
+// (part p takes records p, p+16, ...), two passes (mean, then M2 about it),
+// the 16 partials combined in part order — deterministic, and G/16 dependent
+// adds per thread instead of G/4.
+constexpr int kColParts = 16;
+__global__ void __launch_bounds__(64 * kColParts) col_stats_kernel(const double* __restrict__ rec, int G,
+                                                                   int F, double* __restrict__ st,
+                                                                   int accumulate) {
+  __shared__ double s_n[kColParts][64], s_s[kColParts][64], s_mean[64];
   const int f = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int rl = 1 + 3 * F;
   double n = 0.0, sm = 0.0, q = 0.0;
   double n0 = 0.0, m0 = 0.0, q0 = 0.0;
   if (accumulate && f < F) { n0 = st[0]; m0 = st[1 + f]; q0 = st[1 + F + f]; }
   if (f < F)
-    for (int b = part; b < G; b += 4) {
+    for (int b = part; b < G; b += kColParts) {
       const double nb = rec[(size_t)b * rl];
       n += nb;
       sm += nb * rec[(size_t)b * rl + 1 + f];
@@ -496,14 +609,14 @@ __global__ void __launch_bounds__(256) col_stats_kernel(const double* __restrict
   __syncthreads();
   if (part == 0 && f < F) {
     double N = n0, SM = n0 * m0;
-    for (int p2 = 0; p2 < 4; ++p2) { N += s_n[p2][f]; SM += s_s[p2][f]; }
+    for (int p2 = 0; p2 < kColParts; ++p2) { N += s_n[p2][f]; SM += s_s[p2][f]; }
     s_mean[f] = N > 0 ? SM / N : 0.0;
     s_n[0][f] = N;
   }
   __syncthreads();
   if (f < F) {
     const double mean = s_mean[f];
-    for (int b = part; b < G; b += 4) {
+    for (int b = part; b < G; b += kColParts) {
       const double nb = rec[(size_t)b * rl];
       const double d = rec[(size_t)b * rl + 1 + f] - mean;
       q += rec[(size_t)b * rl + 1 + F + f] + nb * d * d;
@@ -515,7 +628,7 @@ __global__ void __launch_bounds__(256) col_stats_kernel(const double* __restrict
   if (part == 0 && f < F) {
     const double mean = s_mean[f];
     double Q = n0 > 0 ? q0 + n0 * (m0 - mean) * (m0 - mean) : 0.0;
-    for (int p2 = 0; p2 < 4; ++p2) Q += s_s[p2][f];
+    for (int p2 = 0; p2 < kColParts; ++p2) Q += s_s[p2][f];
     if (f == 0) st[0] = s_n[0][0];
     st[1 + f] = mean;
     st[1 + F + f] = Q;
@@ -523,19 +636,20 @@ __global__ void __launch_bounds__(256) col_stats_kernel(const double* __restrict
 }
 
 // column max |x| over the block records (record field 1 + 2F + f), maxed
-// into out[f] when accumulating
-__global__ void __launch_bounds__(256) col_absmax_rec_kernel(const double* __restrict__ rec, int G, int F,
-                                                             float* __restrict__ out, int accumulate) {
-  __shared__ double s_a[4][64];
+// into out[f] when accumulating (a max: any order gives the same value)
+__global__ void __launch_bounds__(64 * kColParts) col_absmax_rec_kernel(const double* __restrict__ rec, int G,
+                                                                        int F, float* __restrict__ out,
+                                                                        int accumulate) {
+  __shared__ double s_a[kColParts][64];
   const int f = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int rl = 1 + 3 * F;
   double a = 0.0;
   if (f < F)
-    for (int b = part; b < G; b += 4) a = fmax(a, rec[(size_t)b * rl + 1 + 2 * F + f]);
+    for (int b = part; b < G; b += kColParts) a = fmax(a, rec[(size_t)b * rl + 1 + 2 * F + f]);
   s_a[part][f] = a;
   __syncthreads();
   if (part == 0 && f < F) {
-    for (int p2 = 1; p2 < 4; ++p2) a = fmax(a, s_a[p2][f]);
+    for (int p2 = 1; p2 < kColParts; ++p2) a = fmax(a, s_a[p2][f]);
     const float v = (float)a;  // a max of floats: exact
     out[f] = accumulate ? fmaxf(out[f], v) : v;
   }
@@ -617,7 +731,7 @@ int mw_nz_stats(const void* d_img, int dtype, int64_t n_pix, int C, double* d_su
       break;
     case MW_U16:
       p = nz_plan<uint16_t>(n_pix, C);
-      hipLaunchKernelGGL(nz_stats_kernel<uint16_t>, dim3(p.G), dim3(256), 0, st,
+      hipLaunchKernelGGL(nz_stats_u16_kernel, dim3(p.G), dim3(256), 0, st,
                          (const uint16_t*)d_img, n_elem, C, p.teff, p.epb, part);
       break;
     case MW_F32:
@@ -630,7 +744,7 @@ int mw_nz_stats(const void* d_img, int dtype, int64_t n_pix, int C, double* d_su
       return MW_EINVAL;
   }
   MW_LAUNCH_CHECK();
-  hipLaunchKernelGGL(nz_stats_reduce, dim3((C + 255) / 256), dim3(256), 0, st, part, p.G, C, d_sum,
+  hipLaunchKernelGGL(nz_stats_reduce, dim3(C), dim3(256), 0, st, part, p.G, C, d_sum,
                      d_cnt);
   MW_LAUNCH_CHECK();
   return MW_OK;
@@ -873,7 +987,7 @@ int mw_blur_assign_conf(const void* d_img, int dtype, int H, int W, int C, const
 int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats, int accumulate,
                           void* stream) {
   MW_CHECK_ARG(d_ws && d_stats && F > 0 && F <= 64, "mw_col_stats_finalize: bad args (F <= 64)");
-  hipLaunchKernelGGL(col_stats_kernel, dim3(1), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(col_stats_kernel, dim3(1), dim3(64 * kColParts), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), stream_blocks(S), F, d_stats, accumulate);
   MW_LAUNCH_CHECK();
   return MW_OK;
@@ -881,7 +995,7 @@ int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats, i
 
 int mw_col_stats_absmax(const void* d_ws, int64_t S, int F, float* d_out, int accumulate, void* stream) {
   MW_CHECK_ARG(d_ws && d_out && S > 0 && F > 0 && F <= 64, "mw_col_stats_absmax: bad args (F <= 64)");
-  hipLaunchKernelGGL(col_absmax_rec_kernel, dim3(1), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(col_absmax_rec_kernel, dim3(1), dim3(64 * kColParts), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), stream_blocks(S), F, d_out, accumulate);
   MW_LAUNCH_CHECK();
   return MW_OK;

@@ -20,12 +20,16 @@ import sys
 KERNELS = {
     "blur": "blur_mfma_kernel<",
     "assign_conf": "assign_kernel<",
-    "kpp_step": "kpp_dist_kernel<32, 4>",
-    "kpp_init": "kpp_dist_kernel<32, 1>",
-    "lloyd_step_mode0": "lloyd_kernel<32, 1, 0>",
-    "lloyd_step_mode1": "lloyd_kernel<32, 1, 1>",
+    "kpp_init": "kpp_pass_kernel<32, 1, 0>",
+    "kpp_step1": "kpp_pass_kernel<32, 4, 1>",
+    "kpp_step": "kpp_pass_kernel<32, 4, 2>",
+    "lloyd_pass_mode0_first": "lloyd_pass_kernel<32, 0, 0, 1>",
+    "lloyd_pass_mode0_tile": "lloyd_pass_kernel<32, 0, 1, 1>",
+    "lloyd_pass_mode1": "lloyd_pass_kernel<32, 1, 0, 1>",
+    "lloyd_pass_mode2": "lloyd_pass_kernel<32, 2, 0, 1>",
     "gather": "gather_kernel<",
     "nz_stats": "nz_stats_kernel<",
+    "mask_scatter": "mask_scatter_kernel",
 }
 UNCALIBRATED = {"gather"}  # 120-B random rows, not a wide coalesced stream
 
