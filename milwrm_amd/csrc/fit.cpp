@@ -427,12 +427,20 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
   bool done = false, strict = false;
   for (int it = 0; it < max_iter && !done; ++it) {
     MW_TRY(fit.upload(centers));
-    int kind = 0;  // first pass
+    static const int first_kind = [] {  // MW_LLOYD_FIRST_ATOMIC=1: LDS-atomic first M-step (A/B)
+      const char* e = getenv("MW_LLOYD_FIRST_ATOMIC");
+      return (e && e[0] == '1') ? 3 : 0;
+    }();
+    static const double queue_below = [] {  // MW_LLOYD_QUEUE_BELOW: kTile/kQueue threshold (A/B)
+      const char* e = getenv("MW_LLOYD_QUEUE_BELOW");
+      return e ? atof(e) : 0.12;
+    }();
+    int kind = first_kind;  // first pass
     if (last_recomputed >= 0) {
       double frac = (double)last_recomputed / (double)S;
       if (fit.prev_dmax > 0.f && std::isfinite(fit.drift_max))
         frac *= std::min(1.0, (double)fit.drift_max / (double)fit.prev_dmax);
-      kind = frac > 0.12 ? 1 : 2;
+      kind = frac > queue_below ? 1 : 2;
     }
     MW_TRY(fit.pass(0, kind, 0, rec));
     for (size_t i = 0; i < (size_t)k * F; ++i) {
