@@ -320,15 +320,29 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
         const int64_t r = c0 + s_q[e0 + (valid ? lane : 0)];
         // gather the batch's rows into the wave tile (row j at s_tile + j*F)
         if ((F & 1) == 0) {
+          // pieces (row j, pair c) = lane + 64 i, in batches of kGB loads in
+          // flight (one load -> store round trip per piece made this phase
+          // latency-bound)
           const int P2 = F >> 1;
           int j = lane / P2, c = lane - (lane / P2) * P2;  // piece (j, c) = p, stepped by 64
           const int dj = 64 / P2, dc = 64 - dj * P2;
-          for (int p = lane; p < 64 * P2; p += 64) {
-            const int64_t rj = c0 + s_q[e0 + (j < cnt_b ? j : 0)];
-            *reinterpret_cast<f2v*>(s_tile + j * F + 2 * c) = *reinterpret_cast<const f2v*>(X + rj * F + 2 * c);
-            j += dj;
-            c += dc;
-            if (c >= P2) { c -= P2; ++j; }
+          constexpr int kGB = 8;
+          for (int i0 = 0; i0 < P2; i0 += kGB) {
+            f2v v[kGB];
+            int dst[kGB];
+#pragma unroll
+            for (int i = 0; i < kGB; ++i) {
+              const bool ok = i0 + i < P2;
+              const int64_t rj = c0 + s_q[e0 + (j < cnt_b ? j : 0)];
+              v[i] = ok ? *reinterpret_cast<const f2v*>(X + rj * F + 2 * c) : f2v{0.f, 0.f};
+              dst[i] = ok ? j * F + 2 * c : -1;
+              j += dj;
+              c += dc;
+              if (c >= P2) { c -= P2; ++j; }
+            }
+#pragma unroll
+            for (int i = 0; i < kGB; ++i)
+              if (dst[i] >= 0) *reinterpret_cast<f2v*>(s_tile + dst[i]) = v[i];
           }
         } else {
           for (int p = lane; p < 64 * F; p += 64) {
