@@ -24,9 +24,11 @@ with contextlib.redirect_stdout(sys.stderr):
     lab = M.mxif_labeler(df)
     lab.prep_cluster_data(features=list(range(30)), sigma=2, fract=0.2)
 rows = lab._rows
-ks = list(range(8, 16))
+ks = list(range(int(os.environ.get("KC_K0", 8)), int(os.environ.get("KC_K1", 16))))
 res = {}
-for name, qb in [("full", -1.0), ("tile", -1.0), ("queue", 2.0), ("mix", 0.12), ("mix3", 0.3)]:
+VARIANTS = [("full", -1.0), ("tile", -1.0), ("queue", 2.0), ("mix", 0.12), ("mix3", 0.3),
+            ("tile2", -1.0), ("queue2", 2.0), ("queue3", 2.0)]
+for name, qb in VARIANTS:
     KM.QUEUE_BELOW = qb
     if name == "full":  # every bound test fails: the plain Lloyd E-step each pass (ground truth)
         os.environ["MW_LLOYD_NOBOUND"] = "1"
@@ -36,7 +38,7 @@ for name, qb in [("full", -1.0), ("tile", -1.0), ("queue", 2.0), ("mix", 0.12), 
         fits = KM.fit_many(rows, ks, random_state=18)
     res[name] = [(np.asarray(m.labels_).copy(), m.cluster_centers_.copy(), m.n_iter_) for m in fits]
 ok = True
-for name in ("tile", "queue", "mix", "mix3"):
+for name in [v for v, _ in VARIANTS[1:]]:
     for i, k in enumerate(ks):
         a, b = res["full"][i], res[name][i]
         same = np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
