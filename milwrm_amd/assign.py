@@ -22,11 +22,11 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
     H, W, C = img_f32.shape
     k, F = centers.shape
     dev = img_f32.device
-    feat = D.h2d(np.asarray(feat_idx, dtype=np.int32), dev)
-    a = D.h2d(np.asarray(inv, dtype=np.float64).astype(np.float32), dev)
-    b = D.h2d((-np.asarray(mu, dtype=np.float64) * np.asarray(inv, dtype=np.float64))
-              .astype(np.float32), dev)
-    c32 = D.h2d(np.asarray(centers, dtype=np.float32), dev)
+    feat, a, b, c32 = D.h2d_many(
+        [np.asarray(feat_idx, dtype=np.int32),
+         np.asarray(inv, dtype=np.float64).astype(np.float32),
+         (-np.asarray(mu, dtype=np.float64) * np.asarray(inv, dtype=np.float64)).astype(np.float32),
+         np.asarray(centers, dtype=np.float32)], dev)
     n = H * W
     lab = torch.empty((H, W), dtype=torch.int8, device=dev) if out_lab is None else out_lab
     conf = torch.empty((H, W), dtype=torch.float32, device=dev) if out_conf is None else out_conf

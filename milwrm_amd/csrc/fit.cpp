@@ -163,6 +163,31 @@ int dev_alloc(DevBuf& b, size_t n) {
   return MW_OK;
 }
 
+// Page-locked staging for the driver's small transfers (one per thread,
+// grown on demand, never freed): copies from pageable std::vectors are staged
+// by the runtime synchronously, ~20 us of host time each, while the GPU waits
+// for the next launch.  Regions: [0, 32K) center tables (H2D), [32K, 160K)
+// pass records (D2H), [160K, 176K) gathered rows (D2H), [176K, 178K) setup
+// arrays (H2D).  Every region is reused only after a stream synchronisation
+// that follows its previous copy.
+constexpr size_t kPinTab = 0, kPinRec = 32 << 10, kPinRows = 160 << 10, kPinSetup = 176 << 10,
+                 kPinIdx = 178 << 10, kPinBytes = 180 << 10;
+static char* pinned_staging() {
+  static thread_local char* p = nullptr;
+  if (!p && hipHostMalloc(reinterpret_cast<void**>(&p), kPinBytes, 0) != hipSuccess) p = nullptr;
+  return p;
+}
+
+// rows X[idx[i]] (idx[0] replaced by `first` when first >= 0) -> out, n x F
+__global__ void rows_gather_kernel(const float* __restrict__ X, int F, const int64_t* __restrict__ idx,
+                                   int64_t first, int n, float* __restrict__ out) {
+  const int i = blockIdx.x, f = threadIdx.x;
+  if (i < n && f < F) {
+    const int64_t r = (i == 0 && first >= 0) ? first : idx[i];
+    out[(size_t)i * F + f] = X[r * F + f];
+  }
+}
+
 struct Fit {
   int64_t S;
   int F, k;
@@ -219,7 +244,13 @@ struct Fit {
     drift_max = dmax;
     prev32.assign(h.begin(), h.begin() + (size_t)k * F);
     have_prev = true;
-    MW_HIP(hipMemcpyAsync(par, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    char* pin = pinned_staging();
+    if (pin && h.size() * sizeof(float) <= kPinRec - kPinTab) {
+      std::memcpy(pin + kPinTab, h.data(), h.size() * sizeof(float));
+      MW_HIP(hipMemcpyAsync(par, pin + kPinTab, h.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    } else {
+      MW_HIP(hipMemcpyAsync(par, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, st));
+    }
     return MW_OK;
   }
 
@@ -238,8 +269,39 @@ struct Fit {
     f.inertia_exp = iexp;
     MW_TRY(mw_lloyd_pass(X, S, F, a32, b32, qexp, 1, &f, mode, kind, st));
     rec.resize(rl);
-    MW_HIP(hipMemcpyAsync(rec.data(), out, rl * sizeof(double), hipMemcpyDeviceToHost, st));
+    char* pin = pinned_staging();
+    if (pin && (size_t)rl * sizeof(double) <= kPinRows - kPinRec) {
+      MW_HIP(hipMemcpyAsync(pin + kPinRec, out, rl * sizeof(double), hipMemcpyDeviceToHost, st));
+      MW_HIP(hipStreamSynchronize(st));
+      std::memcpy(rec.data(), pin + kPinRec, rl * sizeof(double));
+    } else {
+      MW_HIP(hipMemcpyAsync(rec.data(), out, rl * sizeof(double), hipMemcpyDeviceToHost, st));
+      MW_HIP(hipStreamSynchronize(st));
+    }
+    return MW_OK;
+  }
+
+  // the same for indices on the device (idx[0] = first when first >= 0): one
+  // gather kernel into `tmp` (n x F floats of device scratch) and one copy
+  int scaled_rows_dev(const int64_t* d_idx, int64_t first, int n, const double* mu, const double* inv,
+                      float* tmp, std::vector<double>& outv, int64_t* h_idx = nullptr) {
+    char* pin = pinned_staging();
+    const size_t nb = (size_t)n * F * sizeof(float);
+    if (!pin || nb > kPinSetup - kPinRows || n > 64) return -1;
+    hipLaunchKernelGGL(rows_gather_kernel, dim3(n), dim3(64), 0, st, X, F, d_idx, first, n, tmp);
+    MW_HIP(hipGetLastError());
+    MW_HIP(hipMemcpyAsync(pin + kPinRows, tmp, nb, hipMemcpyDeviceToHost, st));
+    if (h_idx) MW_HIP(hipMemcpyAsync(pin + kPinIdx, d_idx, (size_t)n * 8, hipMemcpyDeviceToHost, st));
     MW_HIP(hipStreamSynchronize(st));
+    if (h_idx) {
+      std::memcpy(h_idx, pin + kPinIdx, (size_t)n * 8);
+      if (first >= 0) h_idx[0] = first;
+    }
+    const float* r = reinterpret_cast<const float*>(pin + kPinRows);
+    outv.resize((size_t)n * F);
+    for (int i = 0; i < n; ++i)
+      for (int f = 0; f < F; ++f)
+        outv[(size_t)i * F + f] = ((double)r[(size_t)i * F + f] - mu[f]) * inv[f];
     return MW_OK;
   }
 
@@ -356,10 +418,6 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
     fit.a64[f] = (double)a32[f];
     fit.b64[f] = (double)b32[f];
   }
-  MW_HIP(hipMemcpyAsync(fit.a32, a32.data(), F * 4, hipMemcpyHostToDevice, st));
-  MW_HIP(hipMemcpyAsync(fit.b32, b32.data(), F * 4, hipMemcpyHostToDevice, st));
-  MW_HIP(hipMemcpyAsync(d_mu, h_mu, F * 8, hipMemcpyHostToDevice, st));
-  MW_HIP(hipMemcpyAsync(d_inv, h_inv, F * 8, hipMemcpyHostToDevice, st));
 
   // tolerance: tol * mean over features of the scaled rows' variance
   double tol_abs = 0.0;
@@ -393,7 +451,29 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
     qe[f] = exp_below((double)xmax[f]);
     qscale[f] = std::ldexp(1.0, -qe[f]);
   }
-  MW_HIP(hipMemcpyAsync(fit.qexp, qe.data(), F * 4, hipMemcpyHostToDevice, st));
+  // a32[64] b32[64] qexp[64] absmax[64] | mu64[64] inv64[64]: one copy
+  {
+    std::vector<char> blk(64 * 4 * 4 + 64 * 8 * 2, 0);
+    float* fa = reinterpret_cast<float*>(blk.data());
+    int32_t* qi = reinterpret_cast<int32_t*>(fa + 128);
+    double* dm = reinterpret_cast<double*>(blk.data() + 64 * 4 * 4);
+    for (int f = 0; f < F; ++f) {
+      fa[f] = a32[f];
+      fa[64 + f] = b32[f];
+      qi[f] = qe[f];
+      fa[192 + f] = xmax[f];
+      dm[f] = h_mu[f];
+      dm[64 + f] = h_inv[f];
+    }
+    char* pin = pinned_staging();
+    const void* src = blk.data();
+    if (pin) {
+      std::memcpy(pin + kPinSetup, blk.data(), blk.size());
+      src = pin + kPinSetup;
+    }
+    MW_HIP(hipMemcpyAsync(fit.a32, src, blk.size(), hipMemcpyHostToDevice, st));
+    if (!pin) MW_HIP(hipStreamSynchronize(st));  // pageable source must outlive the copy
+  }
 
   // initial centers
   std::vector<double> centers((size_t)k * F);
@@ -411,11 +491,16 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
     }
     MW_TRY(mw_kpp_indices(big, S, T, k, d_idx, st));
     std::vector<int64_t> idx(k);
-    MW_HIP(hipMemcpyAsync(idx.data(), d_idx, k * 8, hipMemcpyDeviceToHost, st));
-    MW_HIP(hipStreamSynchronize(st));
-    idx[0] = first;
-    MW_TRY(fit.scaled_rows(idx.data(), k, h_mu, h_inv, centers));
-    if (h_init_idx) std::memcpy(h_init_idx, idx.data(), k * sizeof(int64_t));
+    if (fit.scaled_rows_dev(d_idx, first, k, h_mu, h_inv, reinterpret_cast<float*>(d_c64), centers,
+                            idx.data()) == MW_OK) {
+      if (h_init_idx) std::memcpy(h_init_idx, idx.data(), k * sizeof(int64_t));
+    } else {
+      MW_HIP(hipMemcpyAsync(idx.data(), d_idx, k * 8, hipMemcpyDeviceToHost, st));
+      MW_HIP(hipStreamSynchronize(st));
+      idx[0] = first;
+      MW_TRY(fit.scaled_rows(idx.data(), k, h_mu, h_inv, centers));
+      if (h_init_idx) std::memcpy(h_init_idx, idx.data(), k * sizeof(int64_t));
+    }
   }
 
   // Lloyd iterations

@@ -122,6 +122,23 @@ def h2d(a, device=None) -> torch.Tensor:
     return out
 
 
+def h2d_many(arrays, device=None):
+    """Several small host arrays → device in ONE staged copy (16-byte aligned
+    sections of one buffer); returns device views with the arrays' dtypes and
+    shapes."""
+    arrays = [np.ascontiguousarray(a) for a in arrays]
+    offs, n = [], 0
+    for a in arrays:
+        offs.append(n)
+        n += (a.nbytes + 15) & ~15
+    buf = np.zeros(max(n, 16), dtype=np.uint8)
+    for a, o in zip(arrays, offs):
+        buf[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+    dev = h2d(buf, device)
+    return [dev[o:o + a.nbytes].view(torch.from_numpy(a.reshape(-1)[:0]).dtype).view(a.shape)
+            for a, o in zip(arrays, offs)]
+
+
 def h2d_into(dst: torch.Tensor, a) -> None:
     """dst (contiguous device tensor) ← host array of the same size, staged
     like h2d."""
