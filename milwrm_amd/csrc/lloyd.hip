@@ -71,7 +71,10 @@ __device__ __forceinline__ float dist_one(const f2v (&x2)[FMAX / 2], const f2v* 
 // bytes of one wave's row tile (64 rows x FMAX floats)
 __host__ __device__ inline size_t lloyd_tile_bytes(int FMAX) { return (size_t)64 * FMAX * 4; }
 
-constexpr int kChunk = 4096;  // rows per bound-test chunk (kQueue passes): queue of u16 offsets
+#ifndef MW_LLOYD_CHUNK
+#define MW_LLOYD_CHUNK 4096
+#endif
+constexpr int kChunk = MW_LLOYD_CHUNK;  // rows per bound-test chunk (kQueue passes): queue of u16 offsets
 static_assert(kChunk % 1024 == 0, "chunk = whole 4-wave x 256-row groups");
 
 // small per-block LDS state (size a multiple of 16 bytes)
