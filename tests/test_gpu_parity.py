@@ -178,13 +178,18 @@ def test_single_lloyd_step(gpu, golden):
     np.testing.assert_allclose(shift, g["lloyd1_shift"], rtol=1e-3, atol=1e-6)
 
 
-def test_bounded_lloyd_labels_are_argmin(gpu):
+def test_bounded_lloyd_labels_are_argmin(gpu, monkeypatch):
     """The bound-pruned E-step (rows whose bounds prove their label skip the
     distances) gives every row the label of the plain fp32 argmin: after a
     fit, one full E-step (mode 1) with the final centers changes nothing on a
     strictly converged fit, and the labels equal a brute-force argmin."""
+    from milwrm_amd import kmeans as KM
     from milwrm_amd.kmeans import DeviceRows, KMeans, LAST_STATS
 
+    # the Python Lloyd loop records the per-pass statistics read below (the
+    # C driver does not); start from none so no earlier fit's stats leak in
+    monkeypatch.setattr(KM, "USE_C_FIT", False)
+    LAST_STATS.clear()
     rng = np.random.default_rng(3)
     X = np.concatenate([rng.normal(m, 1.0, size=(4000, 12)) for m in (-2, 0, 2, 4)])
     X = (X - X.mean(0)) / X.std(0)
