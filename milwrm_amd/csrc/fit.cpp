@@ -518,7 +518,7 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
     }();
     static const double queue_below = [] {  // MW_LLOYD_QUEUE_BELOW: kTile/kQueue threshold (A/B)
       const char* e = getenv("MW_LLOYD_QUEUE_BELOW");
-      return e ? atof(e) : 0.12;
+      return e ? atof(e) : 0.3;  // as kmeans.QUEUE_BELOW
     }();
     int kind = first_kind;  // first pass
     if (last_recomputed >= 0) {

@@ -276,10 +276,10 @@ __device__ __forceinline__ void load_scaled_row(const float* s_tile, int lane, i
     const f2v* xp = reinterpret_cast<const f2v*>(__builtin_assume_aligned(xs, 8));
 #pragma unroll
     for (int p = 0; p < FMAX / 2; ++p) {
-      // pairs past F would read the next row (or, for the tile's last row,
-      // LDS no pass has written: stale bits, possibly NaN, and NaN * 0 is
-      // NaN) — they are exactly 0 (the padded scaler is 0)
-      x2[p] = 2 * p < F ? __builtin_elementwise_fma(xp[p], sa[p], sb[p]) : f2v{0.f, 0.f};
+      // pairs past F read the next row (finite: times the padded scaler 0
+      // they are exactly 0); the tile's last row reads past 64 * F, which
+      // every caller keeps finite (full tile loads, or zeroed: lloyd kQueue)
+      x2[p] = __builtin_elementwise_fma(xp[p], sa[p], sb[p]);
       // groups of 4 pairs: keeps the scaler reads from all being hoisted
       // (3 x 32 transient VGPRs)
       if ((p & 3) == 3) __builtin_amdgcn_sched_barrier(0);
@@ -287,8 +287,7 @@ __device__ __forceinline__ void load_scaled_row(const float* s_tile, int lane, i
   } else {
 #pragma unroll
     for (int p = 0; p < FMAX / 2; ++p)
-      x2[p] = __builtin_elementwise_fma(f2v{2 * p < F ? xs[2 * p] : 0.f, 2 * p + 1 < F ? xs[2 * p + 1] : 0.f},
-                                        sa[p], sb[p]);
+      x2[p] = __builtin_elementwise_fma(f2v{xs[2 * p], xs[2 * p + 1]}, sa[p], sb[p]);
   }
 }
 

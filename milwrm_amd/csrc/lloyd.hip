@@ -72,7 +72,7 @@ __device__ __forceinline__ float dist_one(const f2v (&x2)[FMAX / 2], const f2v* 
 __host__ __device__ inline size_t lloyd_tile_bytes(int FMAX) { return (size_t)64 * FMAX * 4; }
 
 #ifndef MW_LLOYD_CHUNK
-#define MW_LLOYD_CHUNK 4096
+#define MW_LLOYD_CHUNK 2048  // 4096: 2 blocks per CU (LDS), the sweep's queue passes 15 % slower
 #endif
 constexpr int kChunk = MW_LLOYD_CHUNK;  // rows per bound-test chunk (kQueue passes): queue of u16 offsets
 static_assert(kChunk % 1024 == 0, "chunk = whole 4-wave x 256-row groups");
@@ -248,6 +248,11 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
 
   if constexpr (MODE == 0 && KIND == kQueue) {
     // =========================== queue pass ===========================
+    // the gather writes only the 64 x F floats of a batch; the scaled-row
+    // read of the last row runs past them (padded features, times a zero
+    // scaler), so the rest of the wave's tile buffer must hold finite values,
+    // never stale LDS bits (NaN * 0 = NaN: nondeterministic labels)
+    for (int q = 64 * F + lane; q < 64 * FMAX; q += 64) s_tile[q] = 0.f;
     for (int64_t c0 = lo; c0 < hi; c0 += kChunk) {
       const int clen = (int)min((int64_t)kChunk, hi - c0);
       // ---- phase 1: bound test, 4 consecutive rows per lane, queue the undecided ----

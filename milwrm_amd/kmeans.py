@@ -306,9 +306,10 @@ class _FitState:
 KIND_FIRST, KIND_TILE, KIND_QUEUE = 0, 1, 2
 # a mode-0 pass streams every row (kTile) while the previous pass recomputed
 # more than this fraction of the rows, else only the undecided ones (kQueue):
-# the k = 2..20 sweep at 10k^2 x 30 (tools/sweep_bench.py) took 1.05 / 1.03 /
-# 0.90 s at 0.03 / 0.06 / 0.12
-QUEUE_BELOW = float(os.environ.get("MW_LLOYD_QUEUE_BELOW", "0.12"))
+# the k = 2..20 sweep at 10k^2 x 30 (tools/sweep_bench.py) took 0.77 / 0.69 s
+# at 0.12 / 0.3 (round 1: 1.05 / 1.03 / 0.90 s at 0.03 / 0.06 / 0.12); the
+# single k = 8 fit of the bench is neutral
+QUEUE_BELOW = float(os.environ.get("MW_LLOYD_QUEUE_BELOW", "0.3"))
 # KMeans.fit through the C++ driver (mw_kmeans_fit) where it applies; MW_KMEANS_C=0
 # keeps the Python loop (A/B and the per-pass trace)
 USE_C_FIT = os.environ.get("MW_KMEANS_C", "1") != "0"
