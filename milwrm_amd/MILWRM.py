@@ -464,6 +464,12 @@ class mxif_labeler(tissue_labeler):
                                     xmax_local=D.d2h(xmax))
             self._cluster_host = None
             return
+        # the first image's log-normalise + blur is queued before the host
+        # work below (mask-rank counts, allocations), which then overlaps it
+        batches = list(self.image_df["batch_names"])
+        if images:
+            images[0].log_normalize(mean=means[batches[0]])
+            images[0].blurring(filter_name=filter_name, sigma=sigma)
         # phase 1: mask ranks → sample counts → one preallocated row block
         dev = D.device()
         ranks = [im._mask_rank() for im in images]
@@ -481,8 +487,9 @@ class mxif_labeler(tissue_labeler):
         totals = []
         for n_img, (im, batch, (r2p, M), S) in enumerate(
                 zip(images, self.image_df["batch_names"], ranks, counts)):
-            im.log_normalize(mean=means[batch])
-            im.blurring(filter_name=filter_name, sigma=sigma)
+            if n_img > 0:
+                im.log_normalize(mean=means[batch])
+                im.blurring(filter_name=filter_name, sigma=sigma)
             np.random.seed(16)
             if S:
                 idx, tot = subsample_indices_device(M, fract, 16, dev)

@@ -275,14 +275,24 @@ def mask_rank_async(mask_u8: torch.Tensor):
     ws = WS.get("mrank", N.query("mw_mask_rank_ws_bytes", n))
     with profiling.timed("mask_rank", n):
         N.call("mw_mask_rank", P(mask_u8), n, P(r2p), P(cnt), P(ws), stream())
-    return r2p, cnt
+    # the count comes back by its own copy and event, so reading it later
+    # does not wait for work queued after the rank (e.g. the blur)
+    slot = _PINNED.take(8)
+    slot[1] = _Busy
+    hv = slot[0][:8].view(torch.int64)
+    hv.copy_(cnt, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return r2p, cnt, (slot, hv, ev)
 
 
 def mask_rank(mask_u8: torch.Tensor, pending=None):
     """(rank→pixel int32 tensor of length M, M) for mask != 0 (row-major);
     ``pending`` = an earlier mask_rank_async result for the same mask."""
-    r2p, cnt = mask_rank_async(mask_u8) if pending is None else pending
-    M = int(d2h(cnt)[0])
+    r2p, cnt, (slot, hv, ev) = mask_rank_async(mask_u8) if pending is None else pending
+    ev.synchronize()
+    M = int(hv[0])
+    slot[1] = None
     return r2p[:M], M
 
 

@@ -37,19 +37,36 @@ class DeviceRows:
         self.S, self.F = X.shape
         self.mu = np.zeros(self.F) if mu is None else np.asarray(mu, dtype=np.float64)
         self.inv = np.ones(self.F) if inv is None else np.asarray(inv, dtype=np.float64)
-        dev = X.device
-        self.mu64 = D.h2d(self.mu, dev)
-        self.inv64 = D.h2d(self.inv, dev)
         self.a_host = self.inv.astype(np.float32)
         self.b_host = (-self.mu * self.inv).astype(np.float32)
-        self.a32 = D.h2d(self.a_host, dev)
-        self.b32 = D.h2d(self.b_host, dev)
+        self._dev_affine = None  # (mu64, inv64, a32, b32) on the device, uploaded on first use
         self._feature_var = feature_var
         self.xmax = None      # per-feature max |x| over all rows (all shards)
         # max |x| of this shard's rows when the producer already took it
         # (mw_col_stats_absmax beside the scaler statistics), else a pass
         self._xmax_local = None if xmax_local is None else np.asarray(xmax_local, np.float32)
         self.qexp_dev = None  # fixed-point exponents of the Lloyd M-step (int32, device)
+
+    def _affine(self):
+        if self._dev_affine is None:  # one staged copy (the C fit driver uploads its own)
+            self._dev_affine = D.h2d_many([self.mu, self.inv, self.a_host, self.b_host], self.X.device)
+        return self._dev_affine
+
+    @property
+    def mu64(self):
+        return self._affine()[0]
+
+    @property
+    def inv64(self):
+        return self._affine()[1]
+
+    @property
+    def a32(self):
+        return self._affine()[2]
+
+    @property
+    def b32(self):
+        return self._affine()[3]
 
     def fixed_point(self, comm=None) -> np.ndarray:
         """Exponents e_f with max|x_f| * 2^e_f <= 2^40 (global over the shards
