@@ -34,6 +34,7 @@
 namespace mw {
 
 constexpr int kBlurMfmaMaxR = 8;
+constexpr int kBlurMfmaBH = 512;  // output rows per band (BlurGrid)
 
 typedef float f4m __attribute__((ext_vector_type(4)));
 typedef unsigned int u4m __attribute__((ext_vector_type(4)));
@@ -158,12 +159,13 @@ struct BlurMfmaCfg {
 };
 
 // Band grid: nbx column bands x nby row bands of bh rows, one workgroup each,
-// launched as a 1-D grid (column band fastest).  Measured at 10k^2 x 30
-// (tools/blur_bench.py): 256-row bands 5.29 ms; 128 / 385 / 512 / 770 rows
-// 5.36 / 5.46 / 5.35 / 5.50 ms (fewer, taller bands do not pay despite their
-// smaller halo share); dealing adjacent bands to one XCD (xcd = 1: block b
-// takes logical tile (b % 8) * (tiles / 8) + b / 8) 5.49 ms.  MW_BLUR_BH and
-// MW_BLUR_XCD override both for tuning.
+// launched as a 1-D grid (column band fastest).  Round 2, at 10k^2 x 30
+// (tools/dev/blur_ab.sh, same box, two runs each): 512-row bands 4.72 / 4.74
+// ms vs 256-row 4.79 / 4.81 (the 16 halo rows are 3 % of a 512-row band, 6 %
+// of a 256-row one); 384 / 768 / 1024 rows and 128-column bands slower;
+// dealing adjacent bands to one XCD (xcd = 1: block b takes logical tile
+// (b % 8) * (tiles / 8) + b / 8) slower.  MW_BLUR_BH and MW_BLUR_XCD override
+// both for tuning.
 struct BlurGrid {
   int bh, nbx, ntiles, xcd;
   __device__ __forceinline__ void tile(int b, int G, int& bx, int& by) const {
@@ -177,9 +179,9 @@ struct BlurGrid {
 static inline BlurGrid blur_grid(int H, int nbx) {
   BlurGrid g;
   g.nbx = nbx;
-  g.bh = kBlurBH;
+  g.bh = kBlurMfmaBH;
   g.xcd = 0;
-  if (const char* e = getenv("MW_BLUR_BH")) g.bh = atoi(e) >= 16 ? atoi(e) : kBlurBH;
+  if (const char* e = getenv("MW_BLUR_BH")) g.bh = atoi(e) >= 16 ? atoi(e) : kBlurMfmaBH;
   if (const char* e = getenv("MW_BLUR_XCD")) g.xcd = atoi(e);
   g.ntiles = nbx * ((H + g.bh - 1) / g.bh);
   return g;
