@@ -208,6 +208,23 @@ def estimate_mse_st(cluster_data, adatas, centroids, k):
     return {i: [m[i] for m in per] for i in range(k)}
 
 
+def _check_rows_fit(S: int, F: int, dev) -> None:
+    """The clustering rows of this rank stay in HBM for the whole fit (fp32
+    rows + ~17 bytes of per-row fit state: k-means++ potential, distance
+    bounds, labels).  A cohort whose sampled rows exceed what is free (config
+    5 at 1-2 GPUs: 870 GB of rows) raises here, before any allocation, with the
+    remedy, instead of failing inside a kernel launch."""
+    need = S * (F * 4 + 17)
+    free, _ = torch.cuda.mem_get_info(dev)
+    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)  # torch's cache
+    if need > free:
+        raise MemoryError(
+            f"the {S} clustering rows of this rank ({F} features) need {need / 2**30:.1f} GiB of HBM "
+            f"for the fit and {free / 2**30:.1f} GiB are free: shard the images over more GPUs "
+            f"(comm=milwrm_amd.dist.make_comm() under torchrun; rows are split by image, or one "
+            f"slide by row bands, milwrm_amd.bands) or lower fract")
+
+
 def _assign_img(image: img, features, centers, scaler):
     feats = image._features(features)
     mu, inv = scaler.affine()
@@ -475,6 +492,7 @@ class mxif_labeler(tissue_labeler):
         ranks = [im._mask_rank() for im in images]
         counts = [int(M * fract) for _, M in ranks]
         F = len(images[0]._features(features))
+        _check_rows_fit(sum(counts), F, dev)
         X = torch.empty((sum(counts), F), dtype=torch.float32, device=dev)
         # per-image column statistics [n, mean, M2], merged on the host in
         # image order (comm.merge_image_stats): the same merge sequence for any

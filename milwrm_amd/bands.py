@@ -182,6 +182,9 @@ def prep_banded(image, batch, means, features, filter_name, sigma, fract, comm):
     idx, total = subsample_indices_device(M, fract, 16, dev)
     S = int(idx.shape[0])
     world = b.n_bands
+    from .MILWRM import _check_rows_fit
+
+    _check_rows_fit(S // world + 1, F, dev)
     bnd = owner_bounds(S, world)
     idx64 = idx.to(torch.int64)
     pos, local_idx, send_counts = route_draws(idx64, off, b.band, bnd)

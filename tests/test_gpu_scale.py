@@ -115,3 +115,16 @@ def test_sweep_50_features_equals_separate_fits(gpu):
     ref = O.kmeans_fit(rows.to_host_scaled(), 20, random_state=18)
     assert many[-1].n_iter_ == ref["n_iter_"]
     assert _rel(many[-1].cluster_centers_, ref["cluster_centers_"]) < RTOL
+
+
+def test_rows_beyond_hbm_raise_clearly(gpu, monkeypatch):
+    """Config 5 at 1-2 GPUs: sampled rows beyond the free HBM raise a
+    MemoryError naming the remedy before any allocation (free HBM faked)."""
+    import torch
+
+    from milwrm_amd.MILWRM import _check_rows_fit
+
+    _check_rows_fit(1000, 50, torch.device("cuda", 0))  # small: fine
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (1 << 30, 288 << 30))
+    with pytest.raises(MemoryError, match="shard the images over more GPUs"):
+        _check_rows_fit(4_350_000_000, 50, torch.device("cuda", 0))
