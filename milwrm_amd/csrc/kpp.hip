@@ -213,11 +213,36 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
     if ((F & 1) == 0) {
       // feature pairs as 8-byte LDS reads (conflict-free for 16 lanes; the
       // 4-byte reads of rows F floats apart conflict 2-way for even F)
-#pragma unroll 2
+      // the table entries of the next feature pair are loaded (scalar loads)
+      // while this pair computes: the scalar-cache latency is not exposed
+      // once per pair (same operations in the same order: same bits; 535 ->
+      // 520 us per step pass at config 2, tools/gpu/kvariants.sh)
+      struct TabF { double inv, mi, c[T], pend; };
+      auto ld = [&](int f) {
+        TabF r;
+        const int g = f < 64 ? f : 63;
+        r.inv = tb[g];
+        r.mi = tb[576 + g];
+#pragma unroll
+        for (int c = 0; c < T; ++c) r.c[c] = tb[64 + g * 8 + c];
+        r.pend = MODE == 2 ? tp[g * 8] : 0.0;
+        return r;
+      };
+      auto featt = [&](double xv, const TabF& q) {
+        const double xs = fma(xv, q.inv, -q.mi);
+        xx = fma(xs, xs, xx);
+        if (MODE == 2) dotp = fma(xs, q.pend, dotp);
+#pragma unroll
+        for (int c = 0; c < T; ++c) dot[c] = fma(xs, q.c[c], dot[c]);
+      };
+      TabF t0 = ld(0), t1 = ld(1);
       for (int f = 0; f < FMAX; f += 2) {
+        const TabF n0 = ld(f + 2), n1 = ld(f + 3);
         const f2v x2 = *reinterpret_cast<const f2v*>(xr + f);
-        feat((double)x2.x, f);
-        feat((double)x2.y, f + 1);
+        featt((double)x2.x, t0);
+        featt((double)x2.y, t1);
+        t0 = n0;
+        t1 = n1;
       }
     } else {
 #pragma unroll 4
