@@ -7,8 +7,11 @@ uint8 mask) already resident in HBM:
   → mask rank + legacy-RNG subsample gather + column stats → StandardScaler
   → k-means++ (k=8, random_state=18) → Lloyd to convergence → label +
   confidence pass over every pixel.
-Multi-GPU (torchrun): one slide per rank (weak scaling), pixel-sharded fit
-with RCCL all-reduce of the per-iteration partials (milwrm_amd.dist).
+Multi-GPU: one slide per rank (weak scaling), pixel-sharded fit with RCCL
+all-reduce of the per-iteration partials (milwrm_amd.dist).  Launched either
+by torchrun (WORLD_SIZE set) or as ``bench.py --gpus N``, which spawns the N
+ranks itself (fresh processes, before any GPU call) and fails when fewer than
+N GPUs are visible.
 
 Prints ONE JSON line (rank 0).
 """
@@ -122,11 +125,74 @@ def pmc_traffic(kernel):
     return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT)
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N fresh child processes, one per
+    GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment), each
+    running this script; this parent never touches the GPU (it only counts
+    the devices, which does not initialise HIP on this image) and exits with
+    the first failing child's status.  A child that fails takes the others
+    down (they would wait forever in a collective)."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            c = p.poll()
+            if c is None:
+                continue
+            alive.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in alive:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
+
+
+def check_devices(world: int) -> None:
+    """One GPU per rank on this node: fewer visible devices than ranks is an
+    error, never a silent world-1 run."""
+    have = torch.cuda.device_count()
+    if have < world:
+        print(f"bench.py: {world} ranks (--gpus / WORLD_SIZE) need {world} GPUs on this node, "
+              f"{have} visible", file=sys.stderr, flush=True)
+        sys.exit(2)
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        check_devices(args.gpus)  # before any GPU call
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "--gpus" in " ".join(sys.argv):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    check_devices(local + 1)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

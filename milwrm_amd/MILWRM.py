@@ -28,7 +28,7 @@ from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
 from .dist import LOCAL_COMM
-from .rng import check_total, subsample_indices_device
+from .rng import check_total, set_global_state_after_draws, subsample_indices_device
 
 
 # ------------------------------------------------------------ k selection
@@ -238,10 +238,12 @@ def _assign_img(image: img, features, centers, scaler):
         inv_mean, p = image._pending
         how = os.environ.get("MW_DEFERRED_ASSIGN", "band")
         res = None
-        if how != "fused":
+        band = getattr(image, "_band", None)  # a slide band: label its own rows only
+        out_rows = None if band is None else (band.rows.start, band.rows.stop)
+        if how != "fused" or band is not None:
             res = banded_assign_image(image._device(), sigma, inv_mean, p, feats, mu, inv, centers,
-                                      image._mask_device(), truncate=truncate)
-        if res is None and feats == list(range(image.n_ch)):
+                                      image._mask_device(), truncate=truncate, out_rows=out_rows)
+        if res is None and band is None and feats == list(range(image.n_ch)):
             res = blur_assign_image(image._device(), sigma, inv_mean, p, mu, inv, centers,
                                     image._mask_device(), truncate=truncate)
         if res is not None:
@@ -529,6 +531,7 @@ class mxif_labeler(tissue_labeler):
             self._images = images
         for tot, S in totals:
             check_total(tot, S)
+        set_global_state_after_draws()  # np.random as the reference leaves it (MxIF.py:484-490)
         st = comm.merge_image_stats(D.d2h(img_stats), F)
         self.scaler = StandardScaler.from_stats(st)
         mu, inv = self.scaler.affine()

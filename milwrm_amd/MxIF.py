@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from . import device as D
-from .rng import check_total, subsample_indices_device
+from .rng import check_total, set_global_state_after_draws, subsample_indices_device
 
 
 def checktype(obj):
@@ -379,6 +379,7 @@ class img:
             feat = D.h2d(np.asarray(features, dtype=np.int32), dev)
             D.gather_rows(src, feat, d_idx, r2p, X_out, stats, accumulate)
             check_total(total, S)
+            set_global_state_after_draws()
         return X_out, stats
 
     def subsample_pixels(self, features, fract=0.2, random_state=16):

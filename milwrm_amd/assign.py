@@ -80,15 +80,18 @@ def blur_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: floa
 
 def banded_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
                         inv, centers: np.ndarray, mask_u8: torch.Tensor, truncate: float = 4.0,
-                        band_rows=None):
+                        band_rows=None, out_rows=None):
     """``assign_image(blur(lognorm(raw)))`` for a slide whose fp32 blurred copy
     does not fit HBM: the blur is materialised one band of rows at a time
     (band plus r halo rows of input; the kernel's arithmetic per output value
     does not depend on the band, so labels and confidences are bitwise those
     of the whole-slide blur) into one reused buffer, and each band goes
     through the label pass.  The per-domain sums are added band after band.
-    None when not even a 16-row band fits in half the free HBM."""
+    None when not even a 16-row band fits in half the free HBM.  ``out_rows``
+    = (r0, r1): label only those rows of ``raw`` (a slide band's own rows
+    inside its halo'd array, milwrm_amd.bands); outputs are (r1 - r0) x W."""
     H, W, C = raw.shape
+    r0, r1 = (0, H) if out_rows is None else (int(out_rows[0]), int(out_rows[1]))
     k, F = centers.shape
     w = D.gaussian_taps(sigma, truncate)
     r = (len(w) - 1) // 2
@@ -102,19 +105,20 @@ def banded_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: fl
             band_rows = int(free // 2 // row_bytes) - 2 * r
     if band_rows < 16:
         return None
-    band_rows = min(band_rows, H)
+    band_rows = min(band_rows, r1 - r0)
     dev = raw.device
-    lab = torch.empty((H, W), dtype=torch.int8, device=dev)
-    conf = torch.empty((H, W), dtype=torch.float32, device=dev)
+    lab = torch.empty((r1 - r0, W), dtype=torch.int8, device=dev)
+    conf = torch.empty((r1 - r0, W), dtype=torch.float32, device=dev)
     dom = torch.zeros(2 * k, dtype=torch.float64, device=dev)
     buf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=dev)
-    for y0 in range(0, H, band_rows):
-        y1 = min(H, y0 + band_rows)
+    for y0 in range(r0, r1, band_rows):
+        y1 = min(r1, y0 + band_rows)
         a, b = max(0, y0 - r), min(H, y1 + r)
         out = buf[:b - a]
         D.blur(raw[a:b], sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
-        _, _, d = assign_image(out[y0 - a:y1 - a], feat_idx, mu, inv, centers, mask_u8[y0:y1],
-                               out_lab=lab[y0:y1], out_conf=conf[y0:y1])
+        _, _, d = assign_image(out[y0 - a:y1 - a], feat_idx, mu, inv, centers,
+                               D.padded_mask(mask_u8[y0:y1].contiguous()),
+                               out_lab=lab[y0 - r0:y1 - r0], out_conf=conf[y0 - r0:y1 - r0])
         dom += d
     D.FUSED_USED["assign_banded"] += 1
     return lab, conf, dom
@@ -187,7 +191,10 @@ def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarr
 def domain_sse_rows(X: np.ndarray, centers: np.ndarray, labels) -> dict:
     """``domain_sse_image`` over host rows already in the centers' space (the
     ST estimators' cluster_data): the rows travel as a 1-pixel-wide fp32
-    image, labels < 0 belong to no domain."""
+    image, labels < 0 belong to no domain.  fp32 rows by design (the storage
+    of every clustering row); the sums stay fp64, and the estimators move by
+    ~1e-7 relative against the reference's fp64 rows (tests/test_gpu_qc.py
+    states the tolerance)."""
     X = np.asarray(X, dtype=np.float64)
     S, F = X.shape
     dev = D.device()

@@ -159,16 +159,18 @@ def assemble_rows(recv: torch.Tensor, idx64: torch.Tensor, off, bnd, rank: int) 
 
 def prep_banded(image, batch, means, features, filter_name, sigma, fract, comm):
     """mxif_labeler.prep_cluster_data for one band per rank (module docstring).
-    Returns (X rows of this rank in draw order, per-rank column stats, xmax)."""
+    Returns (X rows of this rank in draw order, per-rank column stats, xmax).
+    A band whose blur is deferred (D.defer_blur: its fp32 blurred copy would
+    not fit beside the raw rows) gathers its sampled rows straight from the
+    fused blur epilogue over the halo'd rows, like the whole-slide path."""
     b = check_group([image], comm)
     dev = D.device()
+    r = int(4.0 * float(sigma) + 0.5)
+    if filter_name == "gaussian" and r > b.halo and b.n_bands > 1:
+        raise ValueError(f"blur radius {r} exceeds the band halo of {b.halo} rows")
     image.log_normalize(mean=means[batch])
     image.blurring(filter_name=filter_name, sigma=sigma)
-    src = D.as_float32(image._materialize())  # band + halo rows, blurred
-    r = int(4.0 * float(sigma) + 0.5)
-    if r > b.halo and b.n_bands > 1:
-        raise ValueError(f"blur radius {r} exceeds the band halo of {b.halo} rows")
-    band_src = src[b.rows]
+    W = int(image.shape[1])
     # mask rank of the band rows, global offsets from the bands above
     mb = D.padded_mask(image._mask_device()[b.rows].contiguous())
     r2p, Mb = D.mask_rank(mb.reshape(-1))
@@ -177,12 +179,12 @@ def prep_banded(image, batch, means, features, filter_name, sigma, fract, comm):
     M = int(off[-1])
     F = len(image._features(features))
     np.random.seed(16)
-    from .rng import subsample_indices_device, check_total
+    from .rng import check_total, set_global_state_after_draws, subsample_indices_device
 
     idx, total = subsample_indices_device(M, fract, 16, dev)
     S = int(idx.shape[0])
     world = b.n_bands
-    from .MILWRM import _check_rows_fit
+    from .MILWRM import _check_rows_fit, _gather_deferred
 
     _check_rows_fit(S // world + 1, F, dev)
     bnd = owner_bounds(S, world)
@@ -191,12 +193,17 @@ def prep_banded(image, batch, means, features, filter_name, sigma, fract, comm):
     rows = torch.empty((int(pos.numel()), F), dtype=torch.float32, device=dev)
     if rows.shape[0]:
         feat = D.h2d(np.asarray(image._features(features), dtype=np.int32), dev)
-        scratch = torch.zeros(1 + 2 * F, dtype=torch.float64, device=dev)
-        D.gather_rows(band_src, feat, local_idx, r2p, rows, scratch, accumulate=False)
+        # pixel index of each band-row rank inside the local (halo'd) array
+        r2p_local = r2p + (b.y0 - b.lo) * W if b.y0 != b.lo else r2p
+        if not _gather_deferred(image, feat, local_idx, r2p_local, rows):
+            src = D.as_float32(image._materialize())  # band + halo rows, blurred
+            scratch = torch.zeros(1 + 2 * F, dtype=torch.float64, device=dev)
+            D.gather_rows(src[b.rows], feat, local_idx, r2p, rows, scratch, accumulate=False)
     # rows move to the rank owning their draw position
     recv = exchange_rows(rows, send_counts, comm)[0] if world > 1 else rows
     X = assemble_rows(recv, idx64, off, bnd, b.band)
     check_total(total, S)
+    set_global_state_after_draws()
     stats = torch.zeros((1, 1 + 2 * F), dtype=torch.float64, device=dev)
     xmax = torch.zeros(F, dtype=torch.float32, device=dev)
     D.col_stats_rows(X, stats[0], accumulate=False, absmax=xmax)

@@ -79,7 +79,10 @@ class DistComm(LocalComm):
     """Collectives on the default process group.  ``device`` is where the
     message tensors live (cuda for RCCL, cpu for gloo tests)."""
 
-    def __init__(self, device=None, group=None):
+    def __init__(self, device=None, group=None, force=False):
+        """``force``: run the sharded code path (every collective) even on a
+        one-rank group -- how the RCCL message path is exercised on a single
+        GPU (tests/test_gpu_nccl.py); results must equal ``LocalComm``'s."""
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -87,14 +90,21 @@ class DistComm(LocalComm):
             device = torch.device("cuda", torch.cuda.current_device()) \
                 if dist.get_backend(group) == "nccl" else torch.device("cpu")
         self.device = device
+        self.force = bool(force)
 
     def sharded(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.force
 
     # -- primitives ------------------------------------------------------
     def all_gather_np(self, a: np.ndarray) -> np.ndarray:
         """[world, *a.shape] in rank order."""
-        t = torch.as_tensor(np.ascontiguousarray(a), device=self.device).contiguous()
+        return self.all_gather_t(torch.as_tensor(np.ascontiguousarray(a)))
+
+    def all_gather_t(self, t: torch.Tensor) -> np.ndarray:
+        """All-gather of a tensor living anywhere (device results stay on the
+        device until the one host copy of the gathered block): [world, *shape]
+        host array in rank order."""
+        t = t.to(self.device).contiguous()
         out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=self.device)
         dist.all_gather_into_tensor(out, t.reshape(-1), group=self.group)
         return out.reshape((self.world,) + tuple(t.shape)).cpu().numpy()
@@ -180,9 +190,13 @@ class DistComm(LocalComm):
         each target ``u_t * pot`` is owned by the first rank whose prefix of
         the best array's local potentials reaches it, and that rank searches
         its shard for ``target - prefix``; the candidates' global indices and
-        raw rows are all-reduced (owner contributes, others zero).  ``engine``
-        holds the local distance arrays (``DeviceKpp``: the mw_kpp_* kernels;
-        tests substitute a host one)."""
+        raw rows travel as ONE all-reduced T x (1 + F) fp64 message (owner
+        contributes, others zero; fp32 rows and indices < 2^53 are exact in
+        fp64).  One host synchronisation per step (the gathered potentials,
+        which the host needs for the targets); the chosen indices and rows
+        stay on the device until the end.  ``engine`` holds the local
+        distance arrays (``DeviceKpp``: the mw_kpp_* kernels; tests substitute
+        a host one)."""
         from .rng import first_center_index, kpp_draws
 
         S, F = rows.S, rows.F
@@ -194,48 +208,43 @@ class DistComm(LocalComm):
         off = int(offs[self.rank])
         u0, steps = kpp_draws(random_state, k, T)
 
-        def rows_of(gidx):
-            """Raw fp32 rows for global indices (owner contributes, all-reduce)."""
-            buf = eng.zeros(len(gidx))
-            for i, g in enumerate(gidx):
-                if g >= 0 and off <= g < off + S:
-                    buf[i] = eng.row(g - off)
-            self.all_reduce_(buf)
-            return buf
-
         first = first_center_index(S_tot, u0)
-        chosen = [first]
-        chosen_rows = [rows_of([first])[0].clone()]
-        eng.init(chosen_rows[0])
-        cand_g = None
-        cand_rows = None
+        msg = self._owned_rows(eng, [first - off if off <= first < off + S else -1], off)
+        chosen = [msg[0, 0]]
+        chosen_rows = [msg[0, 1:]]
+        eng.init(msg[0, 1:].float().contiguous())
+        cand = None
         for c in range(1, k + 1):
             n_arr = 1 if c == 1 else T
-            g = self.all_gather_np(eng.pots(c, n_arr))  # [world, n_arr]
+            g = self.all_gather_t(eng.pots_t(c, n_arr))  # [world, n_arr]: the step's one sync
             tot = np.zeros(n_arr)
             for r in range(self.world):
                 tot = tot + g[r]
             best = int(np.argmin(tot)) if c >= 2 else 0
             if c >= 2:
-                chosen.append(int(cand_g[best]))
-                chosen_rows.append(cand_rows[best].clone())
+                chosen.append(cand[best, 0])
+                chosen_rows.append(cand[best, 1:])
             if c == k:
                 break
             rv_local = kpp_targets(np.asarray(steps[c - 1], dtype=np.float64) * tot[best],
                                    g[:, best], self.rank)
-            loc = eng.search(c, best, rv_local)
-            gsum = torch.from_numpy(np.where(loc >= 0, loc + off, 0).astype(np.int64))
-            self.all_reduce_(gsum)
-            cand_g = gsum.numpy()
-            buf = eng.zeros(T)
-            for t in range(T):
-                if loc[t] >= 0:
-                    buf[t] = eng.row(int(loc[t]))
-            self.all_reduce_(buf)
-            cand_rows = buf
-            eng.trial(c, best, buf)
-        X0 = torch.stack(chosen_rows).double().cpu().numpy()
-        return (X0 - rows.mu) * rows.inv, np.asarray(chosen, dtype=np.int64)
+            cand = self._owned_rows(eng, eng.search_t(c, best, rv_local), off)
+            eng.trial(c, best, cand[:, 1:].float().contiguous())
+        out = torch.cat([torch.stack(chosen)[:, None], torch.stack(chosen_rows)], 1).cpu().numpy()
+        return (out[:, 1:] - rows.mu) * rows.inv, out[:, 0].astype(np.int64)
+
+    def _owned_rows(self, eng, loc, off):
+        """[n, 1 + F] fp64 on the engine's device: (global index, raw row) of
+        the entries this rank owns (``loc`` = local row or -1), summed over the
+        ranks (exactly one owner per entry, zeros elsewhere)."""
+        loc = torch.as_tensor(loc, dtype=torch.int64).to(eng.device)
+        have = loc >= 0
+        X = eng.rows_at(loc.clamp(min=0))
+        X = torch.where(have[:, None], X, torch.zeros_like(X)).double()
+        gi = torch.where(have, loc + off, torch.zeros_like(loc)).double()
+        msg = torch.cat([gi[:, None], X], 1)
+        self.all_reduce_(msg)
+        return msg
 
     # -- empty-cluster relocation --------------------------------------
     def farthest(self, rows, labels, centers_old, n, local_top=None):
@@ -262,12 +271,14 @@ class DistComm(LocalComm):
         sel = g[order]
         far_idx = sel[:, 1].astype(np.int64)
         far_val = sel[:, 0]
-        buf = torch.zeros((n, F + 1), dtype=torch.float64, device=dev)
-        for i, gi in enumerate(far_idx):
-            if off <= gi < off + S:
-                li = int(gi - off)
-                buf[i, :F] = rows.X[li].double()
-                buf[i, F] = float(labels[li].item())
+        # the winners' raw rows and labels from their owners: one message
+        loc = np.where((far_idx >= off) & (far_idx < off + S), far_idx - off, -1)
+        loc_t = torch.as_tensor(loc, dtype=torch.int64, device=dev)
+        have = (loc_t >= 0)[:, None]
+        li = loc_t.clamp(min=0)
+        part = torch.cat([rows.X.index_select(0, li).double(),
+                          torch.as_tensor(labels).to(dev).index_select(0, li).double()[:, None]], 1)
+        buf = torch.where(have, part, torch.zeros_like(part))
         self.all_reduce_(buf)
         b = buf.cpu().numpy()
         xs = (b[:, :F] - rows.mu) * rows.inv
@@ -326,30 +337,32 @@ class DeviceKpp:
         self.rv_dev = torch.empty(T, dtype=torch.float64, device=dev)
         self.loc_dev = torch.empty(T, dtype=torch.int64, device=dev)
 
-    def zeros(self, n):
-        return torch.zeros((n, self.rows.F), dtype=torch.float32, device=self.rows.X.device)
+    @property
+    def device(self):
+        return self.rows.X.device
 
-    def row(self, i):
-        return self.rows.X[i]
+    def rows_at(self, idx: torch.Tensor) -> torch.Tensor:
+        return self.rows.X.index_select(0, idx)
 
     def init(self, center_row):
         r, D = self.rows, self.D
         self.N.call("mw_kpp_init", D.P(r.X), r.S, r.F, D.P(r.mu64), D.P(r.inv64), D.P(center_row),
                     self.T, D.P(self.ws), D.stream())
 
-    def pots(self, c, n_arr):
+    def pots_t(self, c, n_arr) -> torch.Tensor:
         D = self.D
         self.N.call("mw_kpp_pots", D.P(self.ws), self.rows.S, self.T, c, D.P(self.pots_dev),
                     D.stream())
-        return self.pots_dev[:n_arr].cpu().numpy()
+        return self.pots_dev[:n_arr]
 
-    def search(self, c, best, rv_local):
+    def search_t(self, c, best, rv_local) -> torch.Tensor:
+        """Local rows of this rank's targets (-1 where rv_local < 0), on the device."""
         D = self.D
-        self.rv_dev.copy_(torch.from_numpy(rv_local))
+        D.h2d_into(self.rv_dev, np.asarray(rv_local, dtype=np.float64))
         r = self.rows
         self.N.call("mw_kpp_search", D.P(r.X), r.S, r.F, D.P(self.ws), self.T, c, best,
                     D.P(self.rv_dev), D.P(self.loc_dev), D.stream())
-        return self.loc_dev.cpu().numpy()
+        return self.loc_dev
 
     def trial(self, c, best, cand_rows):
         r, D = self.rows, self.D

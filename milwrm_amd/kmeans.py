@@ -274,6 +274,23 @@ def _exp_below(bound: float, bits: int = 40) -> int:
     return bits - int(np.frexp(bound)[1])
 
 
+def _check_fit_memory(rows: DeviceRows, ks) -> None:
+    """HBM for the fits run in lockstep (per fit: uint8 labels + fp32 upper /
+    lower bounds per row, 9 bytes, and its pass workspace), checked before
+    any allocation so a too-large sweep raises with the remedy instead of
+    failing inside torch (find_optimal_k runs 19 fits together)."""
+    S, F = rows.S, rows.F
+    need = sum(S * 9 + N.query("mw_lloyd_ws_bytes", S, k, F) for k in ks)
+    dev = rows.X.device
+    free, _ = torch.cuda.mem_get_info(dev)
+    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    if need > free:
+        raise MemoryError(
+            f"{len(ks)} k-means fits over {S} rows need {need / 2**30:.1f} GiB of HBM for their "
+            f"labels, bounds and workspaces and {free / 2**30:.1f} GiB are free: shard the rows "
+            f"over more GPUs (milwrm_amd.dist) or lower fract")
+
+
 class _FitState:
     """Host side of one Lloyd fit: fp64 centers, exact fixed-point cluster
     sums (int64 hi/lo limbs, value = hi * 2^32 + lo) and sizes, device labels
@@ -386,6 +403,7 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
     qscale = rows.fixed_point(comm)
     a64 = rows.a_host.astype(np.float64)
     b64 = rows.b_host.astype(np.float64)
+    _check_fit_memory(rows, [int(np.asarray(c).shape[0]) for c in inits])
     fits = [_FitState(rows, c, dev) for c in inits]
     ks = [fs.k for fs in fits]
     rls = [N.query("mw_lloyd_rec_len", k, F) for k in ks]
@@ -642,8 +660,11 @@ class KMeans:
                 rs_box.append(as_random_state(self.random_state))
             return rs_box[0]
 
+        # the C driver draws k-means++ from RandomState(seed) itself: an int
+        # seed NumPy accepts (0 <= seed < 2^32; others go through
+        # check_random_state on the Python path and raise as sklearn does)
         seeded_int = isinstance(self.random_state, (int, np.integer)) \
-            and not isinstance(self.random_state, bool)
+            and not isinstance(self.random_state, bool) and 0 <= int(self.random_state) < 2**32
         if (n_init == 1 and not comm.sharded() and not self.verbose and USE_C_FIT
                 and (arraylike or (init == "k-means++" and seeded_int))):
             return self._set_fitted(rows, *self._fit_c(rows, k, init if arraylike else None))
@@ -704,7 +725,8 @@ class KMeans:
             N.call("mw_kmeans_fit", D.P(rows.X), S, F, mu.ctypes.data, inv.ctypes.data,
                    None if var is None else var.ctypes.data,
                    None if xmax is None else xmax.ctypes.data, k,
-                   None if c0 is None else c0.ctypes.data, int(self.random_state or 0) & 0xFFFFFFFF,
+                   None if c0 is None else c0.ctypes.data,
+                   0 if c0 is not None else int(self.random_state),  # unused with an array init
                    int(self.max_iter), float(self.tol or 0.0), D.P(labels), centers.ctypes.data,
                    C.addressof(inertia), C.addressof(n_iter), idx.ctypes.data, D.P(ws), ws.numel(),
                    D.stream())

@@ -67,6 +67,7 @@ def subsample_indices_device(M: int, fract: float, random_state: int = 16, devic
 
     dev = device if device is not None else D.device()
     S = int(M * fract)
+    _LAST_DRAW.clear()
     out = torch.empty(S, dtype=torch.int32, device=dev)
     total = torch.zeros(1, dtype=torch.int64, device=dev)
     if S == 0:
@@ -79,7 +80,50 @@ def subsample_indices_device(M: int, fract: float, random_state: int = 16, devic
     ws = D.WS.get("mtrng", N.query("mw_legacy_randint_gen_ws_bytes", int(M), S, MT_SEGMENT))
     N.call("mw_legacy_randint_from_states", D.P(states), W_avail, int(M), S, MT_SEGMENT, D.P(out),
            D.P(total), D.P(ws), D.stream())
+    _LAST_DRAW.update(M=int(M), S=S, seed=seed, W=int(W), ws=ws, states=states)
     return out, total
+
+
+_LAST_DRAW = {}  # the newest device draw: what the global NumPy state must be advanced past
+
+
+def set_global_state_after_draws() -> None:
+    """Leave NumPy's global RandomState where the reference leaves it after
+    ``np.random.seed(16); np.random.choice(M, S)`` (MxIF.py:484,490): advanced
+    past every 32-bit word the masked rejection consumed (one word per
+    attempt, accepted or not).  From the device generator's per-segment
+    accepted counts (exclusive offsets after its scan) the segment holding the
+    S-th accepted draw is known; its start state is the MT19937 recurrence
+    window after w*L words, i.e. NumPy's key with pos = 624; the host replays
+    at most one segment (L = 79,872 words, ~1 ms) to find the word that
+    accepted draw S came from.  Call after the draw has been synchronised."""
+    import torch
+
+    from . import device as D
+
+    last = dict(_LAST_DRAW)
+    _LAST_DRAW.clear()
+    if not last or last["S"] == 0 or last["M"] < 2:
+        return
+    W, L, S = last["W"], MT_SEGMENT, last["S"]
+    cnt = last["ws"][W * L * 4:W * L * 4 + W * 8].view(torch.int64)
+    off = D.d2h(cnt)
+    w = int(np.searchsorted(off, S - 1, side="right")) - 1
+    need = S - int(off[w])  # accepted draws still needed inside segment w
+    key = D.d2h(last["states"][w * 624:(w + 1) * 624]).view(np.uint32)
+    r = np.uint64(last["M"] - 1)
+    m = r
+    for s in (1, 2, 4, 8, 16):
+        m |= m >> np.uint64(s)
+    rs = np.random.RandomState()
+    rs.set_state(("MT19937", key.copy(), 624))
+    words = rs.randint(0, 2**32, size=L, dtype=np.uint64)  # full range: one word per draw
+    hit = np.nonzero((words & m) <= r)[0]
+    used = int(hit[need - 1]) + 1
+    rs.set_state(("MT19937", key.copy(), 624))
+    if used:
+        rs.randint(0, 2**32, size=used, dtype=np.uint64)
+    np.random.set_state(rs.get_state())
 
 
 _states = {}

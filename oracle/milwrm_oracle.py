@@ -487,10 +487,12 @@ def tissue_id_proportions(tissue_ids, k):
     return counts / counts.sum(axis=0)
 
 
-def create_tissue_mask(img_hwc, features=None, fract=0.2):
+def create_tissue_mask(img_hwc, features=None, fract=0.2, return_gap=False):
     """``img.create_tissue_mask`` (MxIF.py:543-589): lognorm with the
     whole-image channel means, Gaussian sigma 2, subsample, KMeans(2, 18) on
-    unscaled rows, predict all pixels, background flip."""
+    unscaled rows, predict all pixels, background flip.  ``return_gap``: also
+    the per-pixel relative gap (d2 - d1) / d2 of the squared distances to the
+    two centers (the near-tie measure of the 2-means labels)."""
     x = np.asarray(img_hwc, dtype=np.float64)
     h, w, d = x.shape
     x = log_normalize(x, None)
@@ -506,7 +508,13 @@ def create_tissue_mask(img_hwc, features=None, fract=0.2):
         lab = np.where(lab == 0.0, 0.5, lab)
         lab = np.where(lab == 1.0, 0.0, lab)
         lab = np.where(lab == 0.5, 1.0, lab)
-    return lab
+    if not return_gap:
+        return lab
+    xf = x.reshape(h * w, d)
+    dd = np.sort(np.stack([((xf - cc) ** 2).sum(1) for cc in c], 1), axis=1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        gap = ((dd[:, 1] - dd[:, 0]) / dd[:, 1]).reshape(h, w)
+    return lab, gap
 
 
 def confidence_st(X, centers, labels):

@@ -11,7 +11,7 @@ sklearn 1.7.2 / SciPy 1.15.3 / NumPy 2.2.6 numerics.
 Outputs small compressed ``.npz`` fixtures next to this script.  Nothing from
 the reference is copied: the fixtures are inputs and outputs only.
 
-Usage:  python tests/golden/make_golden.py [mxif_small mxif_hard256 preproc_edges st_hex qc]
+Usage:  python tests/golden/make_golden.py [mxif_small mxif_hard256 preproc_edges st_hex qc st_hex_k8]
 """
 from __future__ import annotations
 
@@ -296,6 +296,34 @@ def make_st_hex(MW):
     print("st_hex: k", lab.k, "n_iter", lab.kmeans.n_iter_)
 
 
+def make_st_hex_k8(MW):
+    """Config 1's k (BASELINE.json: "st_labeler ... k=8"): the st_hex sections
+    (same inputs, rebuilt from the same seed) labelled at k = 8 instead of the
+    sweep's k."""
+    rng = np.random.default_rng(11)
+    adatas = []
+    for s, (rows, cols) in enumerate([(50, 55), (48, 52)]):
+        A, coords = _hex_grid(rows, cols)
+        dom = ((coords[:, 0] // 12) * 3 + coords[:, 1] // 14) % 6
+        prof = rng.normal(0, 3, size=(6, 10))
+        pcs = prof[dom] + rng.normal(0, 1.0, size=(coords.shape[0], 10))
+        adatas.append(_DuckAnnData(pcs, A))
+    lab = MW.st_labeler(adatas)
+    lab.prep_cluster_data(use_rep="X_pca", features=None, n_rings=1,
+                          spatial_graph_key="spatial_connectivities", n_jobs=1)
+    lab.label_tissue_regions(k=8, alpha=0.05, plot_out=False, random_state=18, n_jobs=1)
+    lab.confidence_score()
+    out = dict(pcs0=adatas[0].obsm["X_pca"], k=np.array(lab.k),
+               centers=lab.kmeans.cluster_centers_, labels=lab.kmeans.labels_,
+               inertia=np.array(lab.kmeans.inertia_), n_iter=np.array(lab.kmeans.n_iter_),
+               conf0=adatas[0].obs["confidence_score"].values,
+               conf1=adatas[1].obs["confidence_score"].values,
+               tissue_ID1=np.asarray(adatas[1].obs["tissue_ID"].astype(int)),
+               confidence_score_df=lab.confidence_score_df.values.astype(np.float64))
+    np.savez_compressed(os.path.join(HERE, "st_hex_k8.npz"), **out)
+    print("st_hex_k8: n_iter", lab.kmeans.n_iter_)
+
+
 def make_qc(MW, MxIF):
     """Clustering QC and tissue masks through the reference's own functions:
     estimate_percentage_variance_mxif / estimate_mse_mxif (MILWRM.py:280-333,
@@ -378,7 +406,8 @@ def make_qc(MW, MxIF):
 
 if __name__ == "__main__":
     MW, MxIF = _import_reference()
-    which = set(sys.argv[1:]) or {"mxif_small", "mxif_hard256", "preproc_edges", "st_hex", "qc"}
+    which = set(sys.argv[1:]) or {"mxif_small", "mxif_hard256", "preproc_edges", "st_hex", "qc",
+                                   "st_hex_k8"}
     if "mxif_small" in which:
         make_mxif_small(MW, MxIF)
     if "mxif_hard256" in which:
@@ -389,3 +418,5 @@ if __name__ == "__main__":
         make_st_hex(MW)
     if "qc" in which:
         make_qc(MW, MxIF)
+    if "st_hex_k8" in which:
+        make_st_hex_k8(MW)

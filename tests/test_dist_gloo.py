@@ -82,17 +82,15 @@ class _HostKpp:
     squared distances in fp64, sequential cumsum search, first-reach)."""
 
     def __init__(self, rows, T):
+        import torch
+
         self.rows, self.T = rows, T
         self.Xs = rows.scaled()
         self.bank = None
+        self.device = torch.device("cpu")
 
-    def zeros(self, n):
-        import torch
-
-        return torch.zeros((n, self.rows.F), dtype=torch.float32)
-
-    def row(self, i):
-        return self.rows.X[i]
+    def rows_at(self, idx):
+        return self.rows.X.index_select(0, idx)
 
     def _d2(self, raw):
         c = (raw.double().numpy() - self.rows.mu) * self.rows.inv
@@ -101,16 +99,20 @@ class _HostKpp:
     def init(self, center_row):
         self.bank = [self._d2(center_row)]
 
-    def pots(self, c, n_arr):
-        return np.array([self.bank[i].sum() for i in range(n_arr)])
+    def pots_t(self, c, n_arr):
+        import torch
 
-    def search(self, c, best, rv_local):
+        return torch.from_numpy(np.array([self.bank[i].sum() for i in range(n_arr)]))
+
+    def search_t(self, c, best, rv_local):
+        import torch
+
         cum = np.cumsum(self.bank[best])
         out = np.full(self.T, -1, dtype=np.int64)
         for t, rv in enumerate(rv_local):
             if rv >= 0:
                 out[t] = min(int(np.searchsorted(cum, rv)), self.rows.S - 1)
-        return out
+        return torch.from_numpy(out)
 
     def trial(self, c, best, cand_rows):
         base = self.bank[best]

@@ -13,6 +13,7 @@ from oracle import milwrm_oracle as O
 
 pytestmark = pytest.mark.gpu
 FEATS = list(range(8))
+TAU = 1e-5  # near-tie: relative top-2 gap of the squared distances
 
 
 def _preprocessed_imgs(g):
@@ -127,9 +128,27 @@ def test_tissue_id_proportions_mxif(gpu, golden):
     lab.label_tissue_regions(k=4, plot_out=False, random_state=18)
     ax = lab.plot_tissue_ID_proportions_mxif()
     assert ax is not None
-    own = O.tissue_id_proportions([np.nan_to_num(t, nan=-1) for t in lab.tissue_IDs], 4)
+    tids = [np.nan_to_num(t, nan=-1) for t in lab.tissue_IDs]
+    own = O.tissue_id_proportions(tids, 4)
     np.testing.assert_allclose(lab.tissue_ID_proportion.values, own, rtol=1e-12)
-    np.testing.assert_allclose(lab.tissue_ID_proportion.values, g["k4_proportions"], atol=1e-3)
+    # against the reference: every label equal except near-ties (the
+    # reference's own confidence < TAU), and the proportions move by exactly
+    # those pixels
+    ref_t = [np.nan_to_num(t, nan=-1) for t in g["k4_tissue_IDs"]]
+    batches = ["b1", "b1", "b2"]
+    e_p = [O.non_zero_mean(r) for r in g["raw"]]
+    bm = O.batch_means([e for e, _ in e_p], [p for _, p in e_p], batches)
+    moved = 0
+    for i, (r, m, t, tr) in enumerate(zip(g["raw"], g["masks"], tids, ref_t)):
+        pre = O.gaussian_blur(O.log_normalize(r, bm[batches[i]]))
+        cid = O.confidence_mxif(pre, m, FEATS, g["k4_centers"], g["k4_scaler_mean"],
+                                g["k4_scaler_scale"], tr)[0]
+        diff = t != tr
+        assert not (diff & ~(np.nan_to_num(cid, nan=1.0) < TAU)).any(), f"image {i}"
+        moved = max(moved, int(diff.sum()))
+    n_lab = min(int((t >= 0).sum()) for t in ref_t)
+    np.testing.assert_allclose(lab.tissue_ID_proportion.values, g["k4_proportions"],
+                               atol=moved / n_lab + 1e-12)
 
 
 def test_create_tissue_mask_vs_reference(gpu, golden):
@@ -144,7 +163,12 @@ def test_create_tissue_mask_vs_reference(gpu, golden):
         im.create_tissue_mask()
         got = np.asarray(im.mask, dtype=np.float64)
         assert got.shape == ref.shape
-        assert np.mean(got != ref) < 1e-3, np.mean(got != ref)
+        # mismatches only where the 2-means gap of the (pinned) oracle is a
+        # near-tie: relative gap of the squared distances < TAU
+        own, gap = O.create_tissue_mask(r, return_gap=True)
+        np.testing.assert_array_equal(own, ref)  # the oracle reproduces the reference here
+        bad = (got != ref) & ~(np.nan_to_num(gap, nan=0.0) < TAU)
+        assert not bad.any(), f"{int(bad.sum())} mask pixels differ outside near-ties"
     im = M.img(g["raw"][0].copy())
     with pytest.raises(ValueError, match="features"):
         im.create_tissue_mask(features=[0, 1, 2])
@@ -173,6 +197,10 @@ def test_qc_st_vs_reference(gpu, golden):
     offs = np.concatenate([[0], np.cumsum(n_obs)])
     ads = [_Duck(n_obs[s], labels[offs[s]:offs[s + 1]], np.unique(labels)) for s in range(3)]
     pv = [MW.estimate_percentage_variance_st(X[offs[s]:offs[s + 1]], ads[s], cents) for s in range(3)]
+    # tolerance by design: the spots travel to the device as fp32 rows (the
+    # same storage as every clustering row; the reference keeps fp64), which
+    # moves the fp64-accumulated sums by ~1e-7 relative -- inside north_star's
+    # 1e-4 relative bound for fp32
     np.testing.assert_allclose(pv, g["st_pct_variance"], rtol=1e-5)
     mse = MW.estimate_mse_st(X, ads, cents, 5)
     np.testing.assert_allclose(np.array([mse[i] for i in range(5)]), g["st_mse"], rtol=2e-5, atol=1e-9)

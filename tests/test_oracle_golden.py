@@ -202,3 +202,13 @@ def test_create_tissue_mask_oracle(golden):
     g = golden("qc_small")
     for r, ref in zip(g["raw"][:2], g["tissue_mask"]):
         np.testing.assert_array_equal(O.create_tissue_mask(r), ref)
+
+
+def test_st_k8_oracle(golden):
+    """The oracle's KMeans on the st_hex rows at config 1's k = 8 reproduces
+    the reference run at k = 8 (st_hex_k8.npz)."""
+    g, g8 = golden("st_hex"), golden("st_hex_k8")
+    km = O.kmeans_fit(g["cluster_data"], 8, random_state=18)
+    np.testing.assert_array_equal(km["labels_"], g8["labels"])
+    assert km["n_iter_"] == int(g8["n_iter"])
+    np.testing.assert_allclose(km["cluster_centers_"], g8["centers"], rtol=1e-10, atol=1e-12)
