@@ -258,6 +258,9 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
                   void* stream);
 /* per-column max |x| of S x F fp32 rows (F <= 256), fp32 out */
 int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream);
+/* The same maxima folded into d_out (fp32 [F], >= 0) without resetting it:
+ * the column maxima of a slide processed band after band. */
+int mw_col_absmax_acc(const float* d_X, int64_t S, int F, float* d_out, void* stream);
 
 /* ---- whole fit: sklearn KMeans(algorithm="lloyd").fit (_kmeans.py:1427-1554)
  * Replaces the reference's `KMeans(n_clusters=k, random_state=seed).fit(X)`
@@ -325,16 +328,26 @@ int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom,
  * (MILWRM.py:280-333, dc/dm sums), estimate_mse_mxif (MILWRM.py:453-515) and
  * their ST twins estimate_percentage_variance_st / estimate_mse_st
  * (MILWRM.py:518-554, 601-644; rows as a 1-pixel-wide image).
- * Over n_pix HWC fp32 pixels, x' = x[feat[f]]*a[f] + b[f], y = x' - pivot[f] (fp64):
- * d_out (fp64, M = k*F + 2F + k) = [sum over label == d0+d of (x'_f - c_df)^2 (k x F)
- * | sum y_f (F) | sum y_f^2 (F, over every pixel) | pixel count per label (k)].
- * Labels outside [d0, d0+k) (other domains; masked / NaN tissue_ID → -1) add to
- * the sums only.  1 <= k <= 20 domains per call (more: several calls with d0 =
- * 0, 20, 40, ...), 1 <= F <= 256; deterministic (fixed fold order). */
+ * Over n_pix HWC fp32 pixels, x' = x[feat[f]]*a[f] + b[f], y = x' - pivot[f] (fp64).
+ * Exact: every term is rounded once to the fixed point q = rint(v * 2^e) of
+ * its feature (d_qexp, int32 [3F]: e for (x' - c)^2 | for y | for y^2, chosen
+ * by the caller so that |q| <= 2^38) and summed as integers, so the results
+ * do not depend on how the pixels are split over launches (a slide blurred
+ * band by band gives the materialised slide's bits).
+ * d_out (fp64, M = mw_domain_sse_out_len(k, F) = 2(kF + 2F) + k) =
+ * [hi limbs | lo limbs of: sum over label == d0+d of q((x'_f - c_df)^2) (k x F),
+ * sum q(y_f) (F), sum q(y_f^2) (F, over every pixel)] | pixel count per label (k);
+ * value = (hi * 2^32 + lo) * 2^-e.  accumulate != 0 adds to d_out (band after
+ * band) instead of overwriting it.  Labels outside [d0, d0+k) (other
+ * domains; masked / NaN tissue_ID → -1) add to the sums only.  1 <= k <= 20
+ * domains per call (more: several calls with d0 = 0, 20, 40, ...), 1 <= F <=
+ * 256, at most 2^24 pixels per internal block (n_pix <= ~3.4e10). */
+int mw_domain_sse_out_len(int k, int F);
 size_t mw_domain_sse_ws_bytes(int64_t n_pix, int k, int F);
 int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
-                  const double* d_b, const double* d_pivot, const double* d_centers, int k, int d0,
-                  const int8_t* d_label, int64_t n_pix, double* d_out, void* d_ws, void* stream);
+                  const double* d_b, const double* d_pivot, const double* d_centers,
+                  const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
+                  double* d_out, int accumulate, void* d_ws, void* stream);
 
 /* ---- ST feature blur (blur_features_st, ST.py:25-77) --------------------------
  * out[i, f] = mean of X[j, f] over j in (nonzero columns of row i of the CSR

@@ -23,7 +23,7 @@ import torch
 
 from . import device as D
 from .assign import (assign_image, assign_rows, banded_assign_image, blur_assign_image, dm_total,
-                     domain_means, domain_sse_image, domain_sse_rows)
+                     domain_means, domain_sse_deferred, domain_sse_image, domain_sse_rows)
 from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
@@ -149,10 +149,16 @@ def _domain_stats(image, use_path, scaler, centroids, features, tissue_ID):
         image = img.from_npz(image + ".npz")
     feats = image._features(features)
     mu, inv = scaler.affine()
-    # a deferred-blur slide is blurred into a temporary for this pass only
-    src = image._blurred_f32()
-    return domain_sse_image(src, feats, mu, inv, np.asarray(centroids, dtype=np.float64),
-                            tissue_ID)
+    centroids = np.asarray(centroids, dtype=np.float64)
+    if image._pending_blur is not None:
+        # deferred blur (the fp32 blurred slide does not fit HBM): blurred band
+        # by band into a reused buffer; the exact sums make it bitwise the
+        # materialised slide's result
+        sigma, truncate = image._pending_blur
+        inv_mean, p = image._pending
+        return domain_sse_deferred(image._device(), sigma, inv_mean, p, feats, mu, inv, centroids,
+                                   tissue_ID, truncate=truncate)
+    return domain_sse_image(D.as_float32(image._materialize()), feats, mu, inv, centroids, tissue_ID)
 
 
 def estimate_percentage_variance_mxif(image, use_path, scaler, centroids, features, tissue_ID):

@@ -109,23 +109,6 @@ class img:
             self._host64 = None
         return self._device()
 
-    def _blurred_f32(self) -> torch.Tensor:
-        """The preprocessed slide as fp32 for a read-only pass.  A deferred
-        blur (D.defer_blur: the slide did not fit HBM beside its blurred copy)
-        is computed into a temporary that is NOT kept: the img keeps its raw
-        slide and the fused epilogues stay in use."""
-        if self._pending_blur is None:
-            return D.as_float32(self._materialize())
-        sigma, truncate = self._pending_blur
-        inv, p = self._pending
-        src = self._device()
-        need = src.numel() * 4
-        free, _ = torch.cuda.mem_get_info()
-        if need > free:
-            raise MemoryError(f"this pass needs the blurred slide ({need / 2**30:.1f} GiB fp32) and "
-                              f"only {free / 2**30:.1f} GiB of HBM are free")
-        return D.blur(src, sigma, inv_mean=inv, pseudoval=p, truncate=truncate)
-
     def _set_device(self, t: torch.Tensor):
         self._dev = t
         self._host64 = None

@@ -63,6 +63,7 @@ _PROTOS = {
     "mw_lloyd_rec_len": (c_i32, [c_i32, c_i32]),
     "mw_lloyd_pass": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "mw_col_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_col_absmax_acc": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_kmeans_fit_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "mw_kmeans_fit": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_u32, c_i32,
                               C.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
@@ -72,7 +73,9 @@ _PROTOS = {
     "mw_assign_conf": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_reduce": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_domain_sse_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
-    "mw_domain_sse": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "mw_domain_sse_out_len": (c_i32, [c_i32, c_i32]),
+    "mw_domain_sse": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
+                              c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_neighbor_mean": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_col_stats_rows": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_col_stats_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),

@@ -124,12 +124,107 @@ def banded_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: fl
     return lab, conf, dom
 
 
+def _labels_i8(tissue_id, n, k, dev) -> torch.Tensor:
+    """tissue_ID as the kernels read it: int8 per pixel, -1 = no domain."""
+    if isinstance(tissue_id, torch.Tensor) and tissue_id.dtype == torch.int8:
+        return tissue_id.to(dev).reshape(n).contiguous()
+    t = np.asarray(tissue_id, dtype=np.float64).reshape(-1)
+    if t.size != n:
+        raise ValueError(f"tissue_ID has {t.size} pixels, image has {n}")
+    ok = np.isfinite(t) & (t >= 0) & (t < k) & (t == np.floor(t))
+    return D.h2d(np.where(ok, t, -1).astype(np.int8), dev)
+
+
+def _exp38(bound) -> np.ndarray:
+    """Per-entry e with bound * 2^e < 2^38 (the fixed point of mw_domain_sse)."""
+    bound = np.asarray(bound, dtype=np.float64)
+    e = np.zeros(bound.shape, dtype=np.int32)
+    pos = np.isfinite(bound) & (bound > 0)
+    e[pos] = 38 - np.frexp(bound[pos])[1]
+    return e
+
+
+class _DomainSSE:
+    """Exact per-domain QC sums of one slide (mw_domain_sse), accumulated over
+    any number of pixel ranges (the whole slide, or band after band): the
+    fixed point of every feature comes from the slide's column maxima, the
+    scaler, the centers and the pivot, so the sums are the same bits however
+    the pixels are split."""
+
+    def __init__(self, feat, F, mu, inv, centers, pivot, colmax, dev):
+        k = centers.shape[0]
+        if not 1 <= k <= 127:
+            raise ValueError(f"domain statistics support 1 <= k <= 127 domains, got {k}")
+        mu = np.asarray(mu, dtype=np.float64)
+        inv = np.asarray(inv, dtype=np.float64)
+        self.k, self.F, self.dev = k, F, dev
+        b = -mu * inv
+        cen = np.ascontiguousarray(centers, dtype=np.float64)
+        pivot = np.asarray(pivot, dtype=np.float64)
+        # |x'_f| <= |a_f| max|x| + |b_f| (slack for the fp64 rounding of x')
+        xs = (np.abs(inv) * np.asarray(colmax, dtype=np.float64)[feat] + np.abs(b)) * (1 + 1e-12)
+        cm = np.abs(cen).max(axis=0)
+        y = xs + np.abs(pivot)
+        self.exps = np.concatenate([_exp38((xs + cm) ** 2), _exp38(y), _exp38(y * y)]).astype(np.int32)
+        self.pivot = pivot
+        self.chunks = [(d0, min(20, k - d0)) for d0 in range(0, k, 20)]
+        self.feat_d, self.a_d, self.b_d, self.pv_d, self.qe_d = D.h2d_many(
+            [np.asarray(feat, dtype=np.int32), inv, b, pivot, self.exps], dev)
+        self.c_d = [D.h2d(cen[d0:d0 + kc], dev) for d0, kc in self.chunks]
+        self.out = [torch.zeros(N.query("mw_domain_sse_out_len", kc, F), dtype=torch.float64,
+                                device=dev) for _, kc in self.chunks]
+        self.n = 0
+
+    def add(self, img_f32: torch.Tensor, labels_i8: torch.Tensor):
+        """Add the pixels of an HWC fp32 range (and its int8 labels)."""
+        H, W, C = img_f32.shape
+        n = H * W
+        if n == 0:
+            return
+        st = D.stream()
+        for (d0, kc), c_d, out in zip(self.chunks, self.c_d, self.out):
+            ws = D.WS.get("domain_sse", N.query("mw_domain_sse_ws_bytes", n, kc, self.F))
+            with profiling.timed("domain_sse", n * (C * 4 + 1)):
+                N.call("mw_domain_sse", D.P(img_f32), C, D.P(self.feat_d), self.F, D.P(self.a_d),
+                       D.P(self.b_d), D.P(self.pv_d), D.P(c_d), D.P(self.qe_d), kc, d0,
+                       D.P(labels_i8), n, D.P(out), 1, D.P(ws), st)
+        self.n += n
+
+    def result(self) -> dict:
+        F, k = self.F, self.k
+        e = self.exps.astype(np.int64)
+        sse = np.zeros((k, F))
+        count = np.zeros(k)
+        sums = None
+        for (d0, kc), o in zip(self.chunks, D.d2h(*self.out) if len(self.out) > 1 else [D.d2h(self.out[0])]):
+            NQ = kc * F + 2 * F
+            v = o[:NQ] * 4294967296.0 + o[NQ:2 * NQ]
+            scale = np.ldexp(1.0, -np.concatenate([np.tile(e[:F], kc), e[F:2 * F], e[2 * F:]]))
+            v = v * scale
+            sse[d0:d0 + kc] = v[:kc * F].reshape(kc, F)
+            count[d0:d0 + kc] = o[2 * NQ:]
+            if sums is None:
+                sums = (v[kc * F:kc * F + F], v[kc * F + F:])
+        return {"sse": sse, "sum": sums[0], "sumsq": sums[1], "count": count, "n": self.n,
+                "pivot": self.pivot}
+
+
+def _colmax(img_f32: torch.Tensor, out=None, accumulate=False) -> torch.Tensor:
+    H, W, C = img_f32.shape
+    if out is None:
+        out = torch.zeros(C, dtype=torch.float32, device=img_f32.device)
+    if H * W:
+        N.call("mw_col_absmax_acc" if accumulate else "mw_col_absmax", D.P(img_f32), H * W, C,
+               D.P(out), D.stream())
+    return out
+
+
 def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
                      tissue_id, pivot=None) -> dict:
     """Per-domain squared error and whole-slide scaled sums (``mw_domain_sse``;
     the sums behind ``estimate_percentage_variance_mxif`` MILWRM.py:280-333,
     ``estimate_mse_mxif`` :453-515 and the ST twins :518-554, :601-644), one
-    pass per 20 domains.
+    pass per 20 domains, exact (fixed point from the slide's column maxima).
 
     ``tissue_id``: H x W labels as the reference holds them (float, NaN outside
     the mask) or an int8 device map with -1 outside the mask.  ``pivot``: the
@@ -139,53 +234,78 @@ def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarr
     n (pixels), pivot (F)."""
     H, W, C = img_f32.shape
     k, F = centers.shape
-    if not 1 <= k <= 127:
-        raise ValueError(f"domain statistics support 1 <= k <= 127 domains, got {k}")
     img_f32 = img_f32.contiguous()
+    feat = _check_feats(feat_idx, F, C)
+    dev = img_f32.device
+    n = H * W
+    lab = _labels_i8(tissue_id, n, k, dev)
+    if pivot is None:
+        pivot = _first_pixel_scaled(img_f32, feat, mu, inv)
+    acc = _DomainSSE(feat, F, mu, inv, centers, pivot, D.d2h(_colmax(img_f32)), dev)
+    acc.add(img_f32, lab)
+    return acc.result()
+
+
+def _check_feats(feat_idx, F, C) -> np.ndarray:
     feat = np.asarray(feat_idx, dtype=np.int32)
     feat = np.where(feat < 0, feat + C, feat).astype(np.int32)
     if feat.shape != (F,) or feat.min() < 0 or feat.max() >= C:
         raise ValueError(f"features {feat_idx} do not match {F} centroid columns / {C} channels")
-    dev = img_f32.device
-    n = H * W
-    if isinstance(tissue_id, torch.Tensor) and tissue_id.dtype == torch.int8:
-        lab = tissue_id.to(dev).reshape(n).contiguous()
-    else:
-        t = np.asarray(tissue_id, dtype=np.float64).reshape(-1)
-        if t.size != n:
-            raise ValueError(f"tissue_ID has {t.size} pixels, image has {n}")
-        ok = np.isfinite(t) & (t >= 0) & (t < k) & (t == np.floor(t))
-        lab = D.h2d(np.where(ok, t, -1).astype(np.int8), dev)
-    mu = np.asarray(mu, dtype=np.float64)
-    inv = np.asarray(inv, dtype=np.float64)
-    if pivot is None:
-        x0 = D.d2h(img_f32.reshape(n, C)[0]).astype(np.float64)[feat]
-        pivot = x0 * inv - mu * inv
-    a = D.h2d(inv, dev)
-    b = D.h2d(-mu * inv, dev)
-    pv = D.h2d(np.asarray(pivot, dtype=np.float64), dev)
-    feat_d = D.h2d(feat, dev)
-    cen = np.ascontiguousarray(centers, dtype=np.float64)
-    st = D.stream()
-    sse = np.zeros((k, F))
-    count = np.zeros(k)
-    sums = None
-    for d0 in range(0, k, 20):
-        kc = min(20, k - d0)
-        c64 = D.h2d(cen[d0:d0 + kc], dev)
-        M = kc * F + 2 * F + kc
-        out = torch.empty(M, dtype=torch.float64, device=dev)
-        ws = D.WS.get("domain_sse", N.query("mw_domain_sse_ws_bytes", n, kc, F))
-        with profiling.timed("domain_sse", n * (C * 4 + 1)):
-            N.call("mw_domain_sse", D.P(img_f32), C, D.P(feat_d), F, D.P(a), D.P(b), D.P(pv),
-                   D.P(c64), kc, d0, D.P(lab), n, D.P(out), D.P(ws), st)
-        o = D.d2h(out)
-        sse[d0:d0 + kc] = o[:kc * F].reshape(kc, F)
-        count[d0:d0 + kc] = o[kc * F + 2 * F:]
-        if sums is None:
-            sums = (o[kc * F:kc * F + F], o[kc * F + F:kc * F + 2 * F])
-    return {"sse": sse, "sum": sums[0], "sumsq": sums[1], "count": count, "n": n,
-            "pivot": np.asarray(pivot, dtype=np.float64)}
+    return feat
+
+
+def _first_pixel_scaled(img_f32, feat, mu, inv) -> np.ndarray:
+    x0 = D.d2h(img_f32.reshape(-1, img_f32.shape[2])[0]).astype(np.float64)[feat]
+    return x0 * np.asarray(inv, dtype=np.float64) - np.asarray(mu, dtype=np.float64) * np.asarray(
+        inv, dtype=np.float64)
+
+
+def domain_sse_deferred(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
+                        inv, centers: np.ndarray, tissue_id, truncate: float = 4.0,
+                        band_rows=None) -> dict:
+    """``domain_sse_image(blur(lognorm(raw)), ...)`` for a slide whose fp32
+    blurred copy does not fit HBM (the deferred-blur mode): the blur is
+    materialised band by band (band + r halo rows of input) into one reused
+    buffer, twice -- once for the column maxima that fix the fixed point,
+    once for the sums.  The sums are exact, so the result is bitwise the
+    materialised slide's (tests/test_gpu_qc.py)."""
+    H, W, C = raw.shape
+    k, F = centers.shape
+    feat = _check_feats(feat_idx, F, C)
+    w = D.gaussian_taps(sigma, truncate)
+    r = (len(w) - 1) // 2
+    if band_rows is None:
+        env = os.environ.get("MW_ASSIGN_BAND_ROWS")
+        if env:
+            band_rows = int(env)
+        else:
+            free, _ = torch.cuda.mem_get_info()
+            band_rows = int(free // 2 // (W * C * 4)) - 2 * r
+    if band_rows < 1:
+        raise MemoryError("not even one row band of the blurred slide fits in half the free HBM")
+    band_rows = min(band_rows, H)
+    dev = raw.device
+    lab = _labels_i8(tissue_id, H * W, k, dev)
+    buf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=dev)
+
+    def bands():
+        for y0 in range(0, H, band_rows):
+            y1 = min(H, y0 + band_rows)
+            a, b = max(0, y0 - r), min(H, y1 + r)
+            out = buf[:b - a]
+            D.blur(raw[a:b], sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
+            yield y0, y1, out[y0 - a:y1 - a]
+
+    cmax = torch.zeros(C, dtype=torch.float32, device=dev)
+    pivot = None
+    for y0, y1, core in bands():
+        if pivot is None:
+            pivot = _first_pixel_scaled(core, feat, mu, inv)
+        _colmax(core, cmax, accumulate=True)
+    acc = _DomainSSE(feat, F, mu, inv, centers, pivot, D.d2h(cmax), dev)
+    for y0, y1, core in bands():
+        acc.add(core, lab[y0 * W:y1 * W])
+    return acc.result()
 
 
 def domain_sse_rows(X: np.ndarray, centers: np.ndarray, labels) -> dict:

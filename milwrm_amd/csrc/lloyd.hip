@@ -555,22 +555,40 @@ __global__ void __launch_bounds__(256) lloyd_reduce_fits_kernel(const LloydFitsA
 }
 
 // ---- column max |x| (fixed-point exponents of the M-step) ----
+// The launcher makes the grid stride a multiple of F, so each thread walks
+// one residue class of F (its column, computed once) and keeps a register
+// max; one LDS atomic per thread at the end.
 __global__ void __launch_bounds__(256) col_absmax_kernel(const float* __restrict__ X, int64_t S, int F,
                                                          unsigned* __restrict__ out) {
   __shared__ unsigned s_m[256];
   for (int f = threadIdx.x; f < 256; f += blockDim.x) s_m[f] = 0u;
   __syncthreads();
   const int64_t total = S * (int64_t)F;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // element e = row * F + f: each thread walks a fixed residue class of F
-  // only when stride % F == 0; otherwise it recomputes f per element
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const float x = fabsf(X[e]);
-    const int f = (int)(e % F);
-    atomicMax(&s_m[f], __builtin_bit_cast(unsigned, x));  // non-negative floats order as their bits
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // a multiple of F
+  const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int f = (int)(e0 % F);
+  unsigned m = 0u;  // non-negative floats order as their bits
+  int64_t e = e0;
+  for (; e + 3 * stride < total; e += 4 * stride) {
+    const float x0 = fabsf(X[e]), x1 = fabsf(X[e + stride]);
+    const float x2 = fabsf(X[e + 2 * stride]), x3 = fabsf(X[e + 3 * stride]);
+    m = max(m, max(max(__builtin_bit_cast(unsigned, x0), __builtin_bit_cast(unsigned, x1)),
+                   max(__builtin_bit_cast(unsigned, x2), __builtin_bit_cast(unsigned, x3))));
   }
+  for (; e < total; e += stride) m = max(m, __builtin_bit_cast(unsigned, fabsf(X[e])));
+  atomicMax(&s_m[f], m);
   __syncthreads();
-  for (int f = threadIdx.x; f < F; f += blockDim.x) atomicMax(&out[f], s_m[f]);
+  for (int q = threadIdx.x; q < F; q += blockDim.x) atomicMax(&out[q], s_m[q]);
+}
+
+// grid of col_absmax_kernel: <= 2048 blocks, block count a multiple of F / gcd(256, F)
+static int col_absmax_blocks(int64_t total, int F) {
+  int a = 256, b = F;
+  while (b) { const int r = a % b; a = b; b = r; }
+  const int unit = F / a;
+  int nb = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  nb = std::max(unit, (nb / unit) * unit);
+  return nb;
 }
 
 }  // namespace mw
@@ -590,7 +608,20 @@ int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream
   hipStream_t s = as_stream(stream);
   MW_HIP(hipMemsetAsync(d_out, 0, sizeof(float) * F, s));
   const int64_t total = S * (int64_t)F;
-  const int nb = (int)std::min<int64_t>((total + 255) / 256, 2048);
+  const int nb = col_absmax_blocks(total, F);
+  hipLaunchKernelGGL(col_absmax_kernel, dim3(nb), dim3(256), 0, s, d_X, S, F,
+                     reinterpret_cast<unsigned*>(d_out));
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+// max |x| per column folded into d_out (not reset first): a slide's column
+// maxima band after band (the exact QC sums take their fixed point from them)
+int mw_col_absmax_acc(const float* d_X, int64_t S, int F, float* d_out, void* stream) {
+  MW_CHECK_ARG(d_X && d_out && S > 0 && F > 0 && F <= 256, "mw_col_absmax_acc: bad arguments");
+  hipStream_t s = as_stream(stream);
+  const int64_t total = S * (int64_t)F;
+  const int nb = col_absmax_blocks(total, F);
   hipLaunchKernelGGL(col_absmax_kernel, dim3(nb), dim3(256), 0, s, d_X, S, F,
                      reinterpret_cast<unsigned*>(d_out));
   MW_LAUNCH_CHECK();

@@ -13,12 +13,24 @@
 // reference (`tissue_ID == i` is false for NaN).  Domains d0 .. d0+k-1 per
 // launch (label l counts as domain l - d0): more domains take more launches.
 //
+// Exact sums: every fp64 term (the squared error, y, y^2) is rounded once to
+// a per-feature fixed point, q = rint(v * 2^e) with |q| <= 2^38 (the host
+// derives e from the column max |x| of the slide, its scaler and the
+// centers), and summed as int64.  Integer sums do not depend on order, so the
+// statistics are the same bits for any split of the pixels: a slide blurred
+// band by band into a reused buffer (the deferred-blur mode, no full fp32
+// copy) gives exactly the materialised slide's numbers, and so would pixels
+// sharded over GPUs.  Per-block results leave as pairs of integer-valued fp64
+// limbs (hi = floor(v / 2^32), lo = v - hi * 2^32) that the fixed-order fold
+// and any number of band launches add exactly.
+//
 // Layout: a block of 256 threads is split into floor(256/F) groups of F lanes;
 // lane f of a group owns feature f, so a wave reads whole pixels (F contiguous
 // floats for identity features) and every lane keeps its own per-domain
-// column of fp64 accumulators in LDS (no atomics, no bank conflicts); eight
-// pixels' loads are issued before their updates (kQcUnroll = 8).  Per-block partials go to a
-// workspace and a second kernel folds them in a fixed order (deterministic).  HBM-bound: n_pix * (C*4 + 1) bytes.
+// column of int64 accumulators in LDS (no atomics, no bank conflicts); eight
+// pixels' loads are issued before their updates (kQcUnroll = 8).  Per-block
+// partials go to a workspace and a second kernel folds them in a fixed order.
+// HBM-bound: n_pix * (C*4 + 1) bytes.
 #include "common.h"
 
 namespace mw {
@@ -28,36 +40,45 @@ constexpr int kQcMaxK = 20;  // LDS <= 20*256*8 + 2*256*8 + 20*256*4 (F = 1) = 6
 constexpr int kQcMaxBlocks = 2048;
 constexpr int kQcUnroll = 8;
 
+__device__ __forceinline__ long long qc_fix(double v, int e) { return (long long)rint(ldexp(v, e)); }
+
+__device__ __forceinline__ void qc_limbs(long long v, double& hi, double& lo) {
+  const long long h = v >> 32;  // arithmetic shift: floor
+  hi = (double)h;
+  lo = (double)(v - h * (1LL << 32));
+}
+
 __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
     const float* __restrict__ img, int C, const int32_t* __restrict__ feat, int F,
     const double* __restrict__ a, const double* __restrict__ b, const double* __restrict__ pivot,
-    const double* __restrict__ centers, int k, int d0, const int8_t* __restrict__ label, int64_t n_pix,
-    int M, double* __restrict__ part) {
-  extern __shared__ double lds[];
-  double* sse = lds;                                           // [k][256]
-  double* s1s = sse + (size_t)k * kQcThreads;                  // [256]
-  double* s2s = s1s + kQcThreads;                              // [256]
+    const double* __restrict__ centers, const int32_t* __restrict__ qe, int k, int d0,
+    const int8_t* __restrict__ label, int64_t n_pix, int M, double* __restrict__ part) {
+  extern __shared__ long long lds[];
+  long long* sse = lds;                                        // [k][256]
+  long long* s1s = sse + (size_t)k * kQcThreads;               // [256]
+  long long* s2s = s1s + kQcThreads;                           // [256]
   uint32_t* cnt = reinterpret_cast<uint32_t*>(s2s + kQcThreads);  // [k][groups]
   const int t = threadIdx.x;
   const int groups = kQcThreads / F;
   const int g = t / F, f = t - g * F;
-  for (int d = 0; d < k; ++d) sse[d * kQcThreads + t] = 0.0;
+  for (int d = 0; d < k; ++d) sse[d * kQcThreads + t] = 0;
   for (int i = t; i < k * groups; i += kQcThreads) cnt[i] = 0u;
   __syncthreads();
-  double s1 = 0.0, s2 = 0.0;
+  long long s1 = 0, s2 = 0;
   if (g < groups) {
     const int ch = feat[f];
     const double af = a[f], bf = b[f], pf = pivot[f];
+    const int es = qe[f], e1 = qe[F + f], e2 = qe[2 * F + f];
     const int64_t step = (int64_t)gridDim.x * groups;
     auto add = [&](float v, int l) {
       const double x = (double)v * af + bf;
       const double y = x - pf;
-      s1 += y;
-      s2 += y * y;
+      s1 += qc_fix(y, e1);
+      s2 += qc_fix(y * y, e2);
       l -= d0;
       if (l >= 0 && l < k) {
         const double dd = x - centers[l * F + f];
-        sse[l * kQcThreads + t] += dd * dd;
+        sse[l * kQcThreads + t] += qc_fix(dd * dd, es);
         if (f == 0) cnt[l * groups + g] += 1u;
       }
     };
@@ -79,36 +100,46 @@ __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
   s1s[t] = s1;
   s2s[t] = s2;
   __syncthreads();
-  // fold the groups: output [sse k*F | sum F | sumsq F | count k]
-  for (int e = t; e < M; e += kQcThreads) {
-    double r = 0.0;
-    if (e < k * F) {
-      const int d = e / F, ff = e - d * F;
-      for (int gg = 0; gg < groups; ++gg) r += sse[d * kQcThreads + gg * F + ff];
-    } else if (e < k * F + F) {
-      const int ff = e - k * F;
-      for (int gg = 0; gg < groups; ++gg) r += s1s[gg * F + ff];
-    } else if (e < k * F + 2 * F) {
-      const int ff = e - k * F - F;
-      for (int gg = 0; gg < groups; ++gg) r += s2s[gg * F + ff];
+  // fold the groups (int64, exact) and emit limbs:
+  // [sse k*F | sum F | sumsq F] as (hi, lo) pairs, then count k
+  const int NQ = k * F + 2 * F;
+  for (int e = t; e < NQ + k; e += kQcThreads) {
+    if (e < NQ) {
+      long long r = 0;
+      if (e < k * F) {
+        const int d = e / F, ff = e - d * F;
+        for (int gg = 0; gg < groups; ++gg) r += sse[d * kQcThreads + gg * F + ff];
+      } else if (e < k * F + F) {
+        const int ff = e - k * F;
+        for (int gg = 0; gg < groups; ++gg) r += s1s[gg * F + ff];
+      } else {
+        const int ff = e - k * F - F;
+        for (int gg = 0; gg < groups; ++gg) r += s2s[gg * F + ff];
+      }
+      double hi, lo;
+      qc_limbs(r, hi, lo);
+      part[(size_t)blockIdx.x * M + e] = hi;
+      part[(size_t)blockIdx.x * M + NQ + e] = lo;
     } else {
-      const int d = e - k * F - 2 * F;
+      const int d = e - NQ;
+      double r = 0.0;
       for (int gg = 0; gg < groups; ++gg) r += (double)cnt[d * groups + gg];
+      part[(size_t)blockIdx.x * M + 2 * NQ + d] = r;
     }
-    part[(size_t)blockIdx.x * M + e] = r;
   }
 }
 
 // One workgroup per output element: lane i sums blocks i, i+256, ... in order,
-// then a fixed-order block tree (deterministic).
+// then a fixed-order block tree (integer-valued limbs below 2^53: exact).
+// accumulate: add to out (band after band) instead of overwriting it.
 __global__ __launch_bounds__(256) void domain_sse_reduce(const double* __restrict__ part, int G,
-                                                         int M, double* __restrict__ out) {
+                                                         int M, int accumulate, double* __restrict__ out) {
   __shared__ double scratch[256 / kWave];
   const int e = blockIdx.x;
   double r = 0.0;
   for (int i = threadIdx.x; i < G; i += 256) r += part[(size_t)i * M + e];
   r = block_sum(r, scratch);
-  if (threadIdx.x == 0) out[e] = r;
+  if (threadIdx.x == 0) out[e] = accumulate ? out[e] + r : r;
 }
 
 static int qc_blocks(int64_t n_pix, int F) {
@@ -123,30 +154,41 @@ using namespace mw;
 
 extern "C" {
 
+int mw_domain_sse_out_len(int k, int F) { return 2 * (k * F + 2 * F) + k; }
+
 size_t mw_domain_sse_ws_bytes(int64_t n_pix, int k, int F) {
   if (n_pix <= 0 || k <= 0 || F <= 0 || F > kQcThreads) return 0;
-  const int M = k * F + 2 * F + k;
-  return (size_t)qc_blocks(n_pix, F) * M * sizeof(double);
+  return (size_t)qc_blocks(n_pix, F) * mw_domain_sse_out_len(k, F) * sizeof(double);
+}
+
+// the int64 sums are exact while a block's terms (each <= 2^38) stay below 2^62
+static int64_t qc_pixels_per_block(int64_t n_pix, int F) {
+  const int64_t G = qc_blocks(n_pix, F);
+  return (n_pix + G - 1) / G;
 }
 
 int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
-                  const double* d_b, const double* d_pivot, const double* d_centers, int k, int d0,
-                  const int8_t* d_label, int64_t n_pix, double* d_out, void* d_ws, void* stream) {
-  MW_CHECK_ARG(d_img && d_feat && d_a && d_b && d_pivot && d_centers && d_label && d_out && d_ws,
+                  const double* d_b, const double* d_pivot, const double* d_centers,
+                  const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
+                  double* d_out, int accumulate, void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_img && d_feat && d_a && d_b && d_pivot && d_centers && d_qexp && d_label && d_out && d_ws,
                "mw_domain_sse: null pointer");
   MW_CHECK_ARG(n_pix > 0 && C > 0 && F > 0 && F <= kQcThreads && k >= 1 && k <= kQcMaxK && d0 >= 0,
                "mw_domain_sse: bad shape n_pix=%lld C=%d F=%d k=%d d0=%d (F <= 256, k <= 20 per launch)",
                (long long)n_pix, C, F, k, d0);
+  MW_CHECK_ARG(qc_pixels_per_block(n_pix, F) <= (1LL << 24),
+               "mw_domain_sse: %lld pixels per launch exceed the exact int64 sums (split the slide)",
+               (long long)n_pix);
   hipStream_t st = as_stream(stream);
   const int G = qc_blocks(n_pix, F);
-  const int M = k * F + 2 * F + k;
-  const size_t lds = (size_t)k * kQcThreads * sizeof(double) + 2 * kQcThreads * sizeof(double) +
+  const int M = mw_domain_sse_out_len(k, F);
+  const size_t lds = (size_t)k * kQcThreads * sizeof(long long) + 2 * kQcThreads * sizeof(long long) +
                      (size_t)k * (kQcThreads / F) * sizeof(uint32_t);
   double* part = reinterpret_cast<double*>(d_ws);
   hipLaunchKernelGGL(domain_sse_kernel, dim3(G), dim3(kQcThreads), lds, st, d_img, C, d_feat, F,
-                     d_a, d_b, d_pivot, d_centers, k, d0, d_label, n_pix, M, part);
+                     d_a, d_b, d_pivot, d_centers, d_qexp, k, d0, d_label, n_pix, M, part);
   MW_LAUNCH_CHECK();
-  hipLaunchKernelGGL(domain_sse_reduce, dim3(M), dim3(256), 0, st, part, G, M, d_out);
+  hipLaunchKernelGGL(domain_sse_reduce, dim3(M), dim3(256), 0, st, part, G, M, accumulate, d_out);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

@@ -43,13 +43,17 @@ def test_qc_mxif_vs_reference(gpu, golden, k, monkeypatch):
     """estimate_percentage_variance_mxif / estimate_mse_mxif (MILWRM.py:280-333,
     453-515) on the reference's own labelling; k = 24 takes two 20-domain
     passes.  Both blur modes (materialised, and deferred: the QC pass blurs
-    into a temporary and leaves the img's raw slide in place)."""
+    band by band -- 13-row bands here -- into a reused buffer and leaves the
+    img's raw slide in place); the exact fixed-point sums make the two modes
+    BITWISE equal."""
     from milwrm_amd import MILWRM as MW
 
     g = golden("qc_small")
     cents = g[f"k{k}_centers"]
     sc = _scaler(g[f"k{k}_scaler_mean"], g[f"k{k}_scaler_scale"])
     tids = [np.where(t < 0, np.nan, t.astype(np.float64)) for t in g[f"k{k}_tissue_IDs"]]
+    got = {}
+    monkeypatch.setenv("MW_ASSIGN_BAND_ROWS", "13")
     for mode in ("0", "1"):
         monkeypatch.setenv("MW_FUSED_BLUR", mode)
         imgs = _preprocessed_imgs(g)
@@ -57,10 +61,49 @@ def test_qc_mxif_vs_reference(gpu, golden, k, monkeypatch):
               for im, t in zip(imgs, tids)]
         np.testing.assert_allclose(pv, g[f"k{k}_pct_variance"], rtol=1e-5)
         mse = MW.estimate_mse_mxif(imgs, False, tids, sc, cents, FEATS, k)
-        np.testing.assert_allclose(np.array([mse[i] for i in range(k)]), g[f"k{k}_mse"], rtol=2e-5,
-                                   atol=1e-9)
+        mse = np.array([mse[i] for i in range(k)])
+        np.testing.assert_allclose(mse, g[f"k{k}_mse"], rtol=2e-5, atol=1e-9)
+        got[mode] = (np.array(pv), mse)
         if mode == "1":
             assert all(im._pending_blur is not None for im in imgs)  # nothing materialised
+    np.testing.assert_array_equal(got["0"][0], got["1"][0])
+    np.testing.assert_array_equal(got["0"][1], got["1"][1])
+
+
+def test_qc_deferred_50ch_bitwise(gpu, monkeypatch):
+    """50-channel slides (the config-5 channel count): the QC estimators on a
+    deferred-blur slide (band by band, never a full fp32 copy) are bitwise the
+    materialised slide's, and match the oracle's fp64 restatement."""
+    import milwrm_amd as M
+    from milwrm_amd import MILWRM as MW
+
+    raw, mask = O.synth_slide(150, 124, 50, seed=905, mode="hard")
+    rng = np.random.default_rng(3)
+    k = 6
+    mean = raw.reshape(-1, 50).mean(0) + 1.0
+    cents = rng.normal(0, 1, size=(k, 50))
+    sc = _scaler(rng.normal(0.3, 0.05, 50), rng.uniform(0.05, 0.2, 50))
+    tid = rng.integers(-1, k, size=(150, 124)).astype(np.float64)
+    tid[tid < 0] = np.nan
+    res = {}
+    monkeypatch.setenv("MW_ASSIGN_BAND_ROWS", "21")
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MW_FUSED_BLUR", mode)
+        ims = []
+        for j in range(2):
+            im = M.img(raw.copy(), mask=mask.copy())
+            im.log_normalize(mean=mean * (1 + 0.1 * j))
+            im.blurring("gaussian", sigma=2)
+            ims.append(im)
+        assert (ims[0]._pending_blur is not None) == (mode == "1")
+        pv = MW.estimate_percentage_variance_mxif(ims[0], False, sc, cents, list(range(50)), tid)
+        mse = MW.estimate_mse_mxif(ims, False, [tid, tid], sc, cents, list(range(50)), k)
+        res[mode] = (pv, np.array([mse[i] for i in range(k)]))
+    assert res["0"][0] == res["1"][0]
+    np.testing.assert_array_equal(res["0"][1], res["1"][1])
+    pre = O.gaussian_blur(O.log_normalize(raw, mean))
+    ref = O.percentage_variance_mxif(pre, list(range(50)), cents, sc.mean_, sc.scale_, tid)
+    assert abs(res["0"][0] - ref) <= 1e-5 * abs(ref)
 
 
 def test_qc_int8_device_labels_and_single_feature(gpu, golden):
