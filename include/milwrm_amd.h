@@ -329,15 +329,18 @@ int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom,
  * their ST twins estimate_percentage_variance_st / estimate_mse_st
  * (MILWRM.py:518-554, 601-644; rows as a 1-pixel-wide image).
  * Over n_pix HWC fp32 pixels, x' = x[feat[f]]*a[f] + b[f], y = x' - pivot[f] (fp64).
- * Exact: every term is rounded once to the fixed point q = rint(v * 2^e) of
- * its feature (d_qexp, int32 [3F]: e for (x' - c)^2 | for y | for y^2, chosen
- * by the caller so that |q| <= 2^38) and summed as integers, so the results
- * do not depend on how the pixels are split over launches (a slide blurred
- * band by band gives the materialised slide's bits).
- * d_out (fp64, M = mw_domain_sse_out_len(k, F) = 2(kF + 2F) + k) =
- * [hi limbs | lo limbs of: sum over label == d0+d of q((x'_f - c_df)^2) (k x F),
- * sum q(y_f) (F), sum q(y_f^2) (F, over every pixel)] | pixel count per label (k);
- * value = (hi * 2^32 + lo) * 2^-e.  accumulate != 0 adds to d_out (band after
+ * Exact: every term is rounded to the two-level fixed point of its feature,
+ * q = rint(v * 2^e) and r = rint((v * 2^e - q) * 2^38) (d_qexp, int32 [3F]: e
+ * for (x' - c)^2 | for y | for y^2, chosen by the caller so that |q| <= 2^38),
+ * and both levels are summed as integers, so the results do not depend on how
+ * the pixels are split over launches (a slide blurred band by band gives the
+ * materialised slide's bits) and keep ~2^-76 of the bound.
+ * d_out (fp64, M = mw_domain_sse_out_len(k, F) = 4(kF + 2F) + k) =
+ * [Q hi limbs | Q lo limbs | R hi limbs | R lo limbs of the NQ = kF + 2F
+ * quantities: sum over label == d0+d of (x'_f - c_df)^2 (k x F), sum y_f (F),
+ * sum y_f^2 (F, over every pixel)] | pixel count per label (k); with
+ * Q = Qhi * 2^32 + Qlo and R likewise, value = (Q + R * 2^-38) * 2^-e.
+ * accumulate != 0 adds to d_out (band after
  * band) instead of overwriting it.  Labels outside [d0, d0+k) (other
  * domains; masked / NaN tissue_ID → -1) add to the sums only.  1 <= k <= 20
  * domains per call (more: several calls with d0 = 0, 20, 40, ...), 1 <= F <=
@@ -348,6 +351,13 @@ int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const
                   const double* d_b, const double* d_pivot, const double* d_centers,
                   const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
                   double* d_out, int accumulate, void* d_ws, void* stream);
+/* The same over fp64 rows (n_pix x C, row-major): the ST estimators'
+ * cluster_data (estimate_percentage_variance_st / estimate_mse_st,
+ * MILWRM.py:518-554, 601-644), which the reference holds in float64. */
+int mw_domain_sse_f64(const double* d_rows, int C, const int32_t* d_feat, int F, const double* d_a,
+                      const double* d_b, const double* d_pivot, const double* d_centers,
+                      const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
+                      double* d_out, int accumulate, void* d_ws, void* stream);
 
 /* ---- ST feature blur (blur_features_st, ST.py:25-77) --------------------------
  * out[i, f] = mean of X[j, f] over j in (nonzero columns of row i of the CSR

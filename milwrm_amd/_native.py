@@ -76,6 +76,8 @@ _PROTOS = {
     "mw_domain_sse_out_len": (c_i32, [c_i32, c_i32]),
     "mw_domain_sse": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                               c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "mw_domain_sse_f64": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
+                                  c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_neighbor_mean": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_col_stats_rows": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_col_stats_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),

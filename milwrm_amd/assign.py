@@ -176,16 +176,19 @@ class _DomainSSE:
         self.n = 0
 
     def add(self, img_f32: torch.Tensor, labels_i8: torch.Tensor):
-        """Add the pixels of an HWC fp32 range (and its int8 labels)."""
+        """Add the pixels of an HWC fp32 range (or fp64 rows as an S x 1 x F
+        image) and its int8 labels."""
         H, W, C = img_f32.shape
         n = H * W
         if n == 0:
             return
         st = D.stream()
+        f64 = img_f32.dtype == torch.float64
         for (d0, kc), c_d, out in zip(self.chunks, self.c_d, self.out):
             ws = D.WS.get("domain_sse", N.query("mw_domain_sse_ws_bytes", n, kc, self.F))
-            with profiling.timed("domain_sse", n * (C * 4 + 1)):
-                N.call("mw_domain_sse", D.P(img_f32), C, D.P(self.feat_d), self.F, D.P(self.a_d),
+            with profiling.timed("domain_sse", n * (C * img_f32.element_size() + 1)):
+                N.call("mw_domain_sse_f64" if f64 else "mw_domain_sse", D.P(img_f32), C, D.P(self.feat_d),
+                       self.F, D.P(self.a_d),
                        D.P(self.b_d), D.P(self.pv_d), D.P(c_d), D.P(self.qe_d), kc, d0,
                        D.P(labels_i8), n, D.P(out), 1, D.P(ws), st)
         self.n += n
@@ -198,11 +201,13 @@ class _DomainSSE:
         sums = None
         for (d0, kc), o in zip(self.chunks, D.d2h(*self.out) if len(self.out) > 1 else [D.d2h(self.out[0])]):
             NQ = kc * F + 2 * F
-            v = o[:NQ] * 4294967296.0 + o[NQ:2 * NQ]
+            # two-level fixed point: (hi + lo 2^-38) 2^-e, each level as 32-bit limbs
+            hi = o[:NQ] * 4294967296.0 + o[NQ:2 * NQ]
+            lo = o[2 * NQ:3 * NQ] * 4294967296.0 + o[3 * NQ:4 * NQ]
             scale = np.ldexp(1.0, -np.concatenate([np.tile(e[:F], kc), e[F:2 * F], e[2 * F:]]))
-            v = v * scale
+            v = (hi + np.ldexp(lo, -38)) * scale
             sse[d0:d0 + kc] = v[:kc * F].reshape(kc, F)
-            count[d0:d0 + kc] = o[2 * NQ:]
+            count[d0:d0 + kc] = o[4 * NQ:]
             if sums is None:
                 sums = (v[kc * F:kc * F + F], v[kc * F + F:])
         return {"sse": sse, "sum": sums[0], "sumsq": sums[1], "count": count, "n": self.n,
@@ -220,7 +225,7 @@ def _colmax(img_f32: torch.Tensor, out=None, accumulate=False) -> torch.Tensor:
 
 
 def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
-                     tissue_id, pivot=None) -> dict:
+                     tissue_id, pivot=None, colmax=None) -> dict:
     """Per-domain squared error and whole-slide scaled sums (``mw_domain_sse``;
     the sums behind ``estimate_percentage_variance_mxif`` MILWRM.py:280-333,
     ``estimate_mse_mxif`` :453-515 and the ST twins :518-554, :601-644), one
@@ -231,7 +236,8 @@ def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarr
     shift of the whole-slide sums (default: the scaled features of the first
     pixel, which keeps a near-constant feature free of cancellation).  Returns
     fp64 host arrays: sse (k x F), sum / sumsq of x' - pivot (F), count (k),
-    n (pixels), pivot (F)."""
+    n (pixels), pivot (F).  ``colmax``: the per-channel max |x| (default: a
+    device pass over the fp32 slide)."""
     H, W, C = img_f32.shape
     k, F = centers.shape
     img_f32 = img_f32.contiguous()
@@ -241,7 +247,9 @@ def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarr
     lab = _labels_i8(tissue_id, n, k, dev)
     if pivot is None:
         pivot = _first_pixel_scaled(img_f32, feat, mu, inv)
-    acc = _DomainSSE(feat, F, mu, inv, centers, pivot, D.d2h(_colmax(img_f32)), dev)
+    if colmax is None:
+        colmax = D.d2h(_colmax(img_f32))
+    acc = _DomainSSE(feat, F, mu, inv, centers, pivot, colmax, dev)
     acc.add(img_f32, lab)
     return acc.result()
 
@@ -310,19 +318,16 @@ def domain_sse_deferred(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: fl
 
 def domain_sse_rows(X: np.ndarray, centers: np.ndarray, labels) -> dict:
     """``domain_sse_image`` over host rows already in the centers' space (the
-    ST estimators' cluster_data): the rows travel as a 1-pixel-wide fp32
-    image, labels < 0 belong to no domain.  fp32 rows by design (the storage
-    of every clustering row); the sums stay fp64, and the estimators move by
-    ~1e-7 relative against the reference's fp64 rows (tests/test_gpu_qc.py
-    states the tolerance)."""
-    X = np.asarray(X, dtype=np.float64)
+    ST estimators' cluster_data): the rows travel as a 1-pixel-wide fp64
+    image (``mw_domain_sse_f64``: the reference's float64 rows, no fp32
+    rounding), labels < 0 belong to no domain."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
     S, F = X.shape
     dev = D.device()
-    img = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32).reshape(S, 1, F)).to(dev)
+    img = torch.from_numpy(X.reshape(S, 1, F)).to(dev)
     lab = torch.from_numpy(np.asarray(labels, dtype=np.int64).clip(-1, 127).astype(np.int8)).to(dev)
-    x0 = X[0].astype(np.float32).astype(np.float64)
     return domain_sse_image(img, np.arange(F), np.zeros(F), np.ones(F), centers, lab.reshape(S, 1),
-                            pivot=x0)
+                            pivot=X[0].copy(), colmax=np.abs(X).max(axis=0) if S else np.zeros(F))
 
 
 def dm_total(s: dict) -> np.float64:

@@ -115,7 +115,7 @@ __device__ __forceinline__ void vm_wait_n() {
 // bytes) through the raw DMA ring: each ring slot carries one more 1-KB DMA
 // piece past the raw input row, with the side data of the output row that the
 // same slot serves.
-template <typename T, int R, int CT, int BT, int EPI = kEpiStore>
+template <typename T, int R, int CT, int BT, int EPI = kEpiStore, bool H16 = false>
 struct BlurMfmaCfg {
   static constexpr int NR = 2 * R + 1;
   static constexpr int BW = 16 * BT;            // output columns per band
@@ -125,7 +125,15 @@ struct BlurMfmaCfg {
   static constexpr int NK = (16 + 2 * R + 3) / 4;  // MFMA k-steps (4 input columns each)
   static constexpr int NT = 64 * BT * CT;
   static constexpr int NW = NT / 64;
-  static constexpr int ROW = NPX * PS;          // floats per LDS fp32 row buffer
+  // H16 (log-normalised input): the row is held as two f16 images, hi and lo
+  // (x = hi + lo to 2^-22), each [pixel slot][U units of 16 channels] with the
+  // units XOR-swizzled by slot (blur_h16_unit) so that the transposed operand
+  // reads are conflict-free; NPXS slots are read by the K = 32 operand of the
+  // last tile (BW + 16 >= NPX), slot NPXS is the sink of pad pairs
+  static constexpr int U = CT <= 2 ? 2 : 4;
+  static constexpr int NPXS = BW + 16;
+  static constexpr int IMGH = (NPXS + 1) * U * 16;  // halves per f16 image
+  static constexpr int ROW = H16 ? IMGH : NPX * PS;  // floats per LDS row buffer (H16: hi + lo images)
   static constexpr int STG = BW * 16 * CT;      // floats per LDS output staging row (>= BW*C)
   // raw input row segment: <= NPX * C elements, C <= 16*CT, fetched as NPC
   // lane-linear 1-KB DMA pieces (piece i: wave i % NW, round i / NW); the
@@ -158,6 +166,30 @@ struct BlurMfmaCfg {
   static constexpr size_t lds_bytes() { return FIXED + (size_t)D * SLOT; }
 };
 
+typedef _Float16 h2m __attribute__((ext_vector_type(2)));
+typedef _Float16 h8m __attribute__((ext_vector_type(8)));
+typedef short s4m __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4m lds_s4m;
+
+// H16 image: physical 16-channel unit of channel tile ct in pixel slot x.  A
+// transposed read (ds_read_b64_tr_b16) of the 16x16x32 B operand takes, per
+// 32-lane half, slots 8n..8n+3 and 8n+8..8n+11 (4 lanes x 8 bytes each): with
+// U = 2 units per slot the slot bit 3 flips the unit, with U = 4 slot bits 1
+// and 3 do, and the 32 lanes cover all 64 banks exactly once.
+template <int U>
+__host__ __device__ __forceinline__ int blur_h16_unit(int x, int ct) {
+  return U == 2 ? ct ^ ((x >> 3) & 1) : ct ^ (((x >> 1) & 1) | (((x >> 3) & 1) << 1));
+}
+// log-normalised values are scaled by 2^8 before the split (the lo half stays
+// clear of f16 subnormals), the horizontal taps by 2^16; the vertical taps
+// take the 2^-24 back (exact: powers of two)
+#ifdef MW_BLUR_F32H
+constexpr bool kBlurH16 = false;  // A/B builds: horizontal pass on the f32 matrix cores
+#else
+constexpr bool kBlurH16 = true;   // log-normalised input: horizontal pass on f16 hi/lo products
+#endif
+constexpr float kH16XS = 256.f, kH16TS = 65536.f, kH16VS = 1.f / 16777216.f;
+
 // Band grid: nbx column bands x nby row bands of bh rows, one workgroup each,
 // launched as a 1-D grid (column band fastest).  Round 2, at 10k^2 x 30
 // (tools/dev/blur_ab.sh, same box, two runs each): 512-row bands 4.72 / 4.74
@@ -188,13 +220,15 @@ static inline BlurGrid blur_grid(int H, int nbx) {
 }
 
 template <typename T, int R, int CT, int BT, bool LOGN, int EPI>
-__global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_mfma_kernel(const T* __restrict__ in, int H, int W,
+__global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __restrict__ in, int H, int W,
                                                                  int C, const float* __restrict__ inv_mean,
                                                                  float pseudo, BlurTaps taps,
                                                                  float* __restrict__ out, BlurEpi ep,
                                                                  BlurGrid bg) {
-  using K = BlurMfmaCfg<T, R, CT, BT, EPI>;
+  constexpr bool H16 = LOGN && kBlurH16;
+  using K = BlurMfmaCfg<T, R, CT, BT, EPI, H16>;
   constexpr int NS = K::NS, KS = kEpiKS;
+  constexpr int U = K::U, IMGH = K::IMGH, NPXS = K::NPXS;
   constexpr int NR = K::NR, BW = K::BW, NPX = K::NPX, PS = K::PS, NK = K::NK, NT = K::NT;
   constexpr int ROW = K::ROW, STG = K::STG, NCH = K::NCH, NP = K::NP, CP = Chunk16<T>::P;
   constexpr int NG = K::NG, SLOT = K::SLOT, D = K::D, LA = K::LA;
@@ -248,7 +282,10 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
       const int px = ok ? (int)(e / (uint32_t)C) : 0;
       const int ch = ok ? (int)(e - (uint32_t)px * C) : 0;
       const int col = col_a + px, ctile = ch >> 4;
-      p_dst[c * CP + i] = ok ? col * PS + 16 * (SWZ ? (ctile ^ (col & 1)) : ctile) + (ch & 15) : -1;
+      if constexpr (H16)  // byte offset in an f16 image (pad pairs: the sink slot)
+        p_dst[c * CP + i] = 2 * (ok ? col * U * 16 + 16 * blur_h16_unit<U>(col, ctile) + (ch & 15) : NPXS * U * 16);
+      else
+        p_dst[c * CP + i] = ok ? col * PS + 16 * (SWZ ? (ctile ^ (col & 1)) : ctile) + (ch & 15) : -1;
       p_inv[c * CP + i] = (LOGN && ok) ? bf2{inv_mean[ch], inv_mean[ch + 1]} : bf2{1.f, 1.f};
     }
   }
@@ -266,10 +303,34 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
   const int m = lane & 15, kq = lane >> 4;
   float a_op[NK];
   const float tap_scale = LOGN ? 0.30102999566398120f : 1.f;  // log2 -> log10 (log2norm2)
+  if constexpr (!H16) {
 #pragma unroll
-  for (int st = 0; st < NK; ++st) {
-    const int j = 4 * st + kq - m;
-    a_op[st] = (j >= 0 && j <= 2 * R) ? taps.w[j] * tap_scale : 0.f;
+    for (int st = 0; st < NK; ++st) {
+      const int j = 4 * st + kq - m;
+      a_op[st] = (j >= 0 && j <= 2 * R) ? taps.w[j] * tap_scale : 0.f;
+    }
+  }
+  // H16: A[m][k = 8kq + i] = tap k - m (x 2^16, split hi + lo); B = rows of the
+  // hi / lo images by two transposed reads each (slots 16tx + 8kq + 4r + q,
+  // channels 16ct + 4p .. +3 from lane 4q + p of the group)
+  h8m a_hi, a_lo;
+  uint32_t b_addr[2] = {0u, 0u};
+  if constexpr (H16) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int j = 8 * kq + i - m;
+      // taps arrive x 2^-24 (the vertical pass's descale, launch_blur_mfma_one)
+      const float w = (j >= 0 && j <= 2 * R) ? taps.w[j] * (tap_scale * kH16TS * 16777216.f) : 0.f;
+      const _Float16 h = (_Float16)w;
+      a_hi[i] = h;
+      a_lo[i] = (_Float16)(w - (float)h);
+    }
+    const int q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int x = 16 * tx + 8 * kq + 4 * r + q;
+      b_addr[r] = lds_addr_u32(s_rows) + 2u * (uint32_t)(x * U * 16 + 16 * blur_h16_unit<U>(x, ct) + 4 * p);
+    }
   }
   // B[k][n] for k-step st: column 16*tx + 4*st + kq, channel 16*ct + n (n = m)
   const int b_ct = SWZ ? (ct ^ (kq & 1)) : ct;  // (16*tx + 4*st + kq) & 1 == kq & 1
@@ -354,6 +415,20 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
 #pragma unroll
       for (int i = 0; i < CP; ++i) {
         bf2 x = Chunk16<T>::pair(v, i);
+        if constexpr (H16) {
+          // x * 2^8 = hi + lo, both f16 (hi round-to-nearest, the residual exact in fp32)
+#ifdef MW_ABL_NOCONV
+          const h2m h = __builtin_convertvector(x, h2m), l = h;  // ablation: no log, no split
+#else
+          x = log2norm2(x, p_inv[c * CP + i], pseudo) * bf2{kH16XS, kH16XS};
+          const h2m h = __builtin_convertvector(x, h2m);
+          const h2m l = __builtin_convertvector(x - __builtin_convertvector(h, bf2), h2m);
+#endif
+          char* img = reinterpret_cast<char*>(dst) + p_dst[c * CP + i];
+          *reinterpret_cast<h2m*>(img) = h;
+          *reinterpret_cast<h2m*>(img + 2 * IMGH) = l;
+          continue;
+        }
 #ifndef MW_X_NOLOG
         if (LOGN) x = log2norm2(x, p_inv[c * CP + i], pseudo);  // log10(2): in the taps
 #endif
@@ -361,7 +436,18 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
         *reinterpret_cast<bf2*>(d >= 0 ? dst + d : s_dummy) = x;  // pad pairs: the sink
       }
     }
-    if (edge) {  // clamped halo columns ('nearest'): copies of the edge column
+    if (H16 && edge) {  // clamped halo columns: copies of the edge column, both images
+      lds_barrier();
+      const int nl = col_a, nr = NPX - (col_a + (xb - xa));
+      uint32_t* img = reinterpret_cast<uint32_t*>(dst);
+      for (int q2 = t; q2 < (nl + nr) * CT * 8 * 2; q2 += NT) {
+        const int im = q2 & 1, f = (q2 >> 1) & 7, u = (q2 >> 4) % CT, h = (q2 >> 4) / CT;
+        const int col = h < nl ? h : col_a + (xb - xa) + (h - nl);
+        const int src = h < nl ? col_a : col_a + (xb - xa) - 1;
+        const int o = im * IMGH / 2;  // in pairs
+        img[o + col * U * 8 + 8 * blur_h16_unit<U>(col, u) + f] = img[o + src * U * 8 + 8 * blur_h16_unit<U>(src, u) + f];
+      }
+    } else if (edge) {  // clamped halo columns ('nearest'): copies of the edge column
       lds_barrier();
       const int nl = col_a, nr = NPX - (col_a + (xb - xa));
       for (int q2 = t; q2 < (nl + nr) * PS; q2 += NT) {
@@ -473,18 +559,36 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
   auto step = [&](const int s, const int j, const bool guard) {
     if (!guard || s + 1 < nrows) convert_row(s + 1);
     float b_op[NK];
+    h8m b_hi, b_lo;
     if (!guard || s < nrows) {
-      const float* rowp = s_rows + (s & 1) * ROW + b_base;
+      if constexpr (H16) {
+        const uint32_t bo = (uint32_t)(s & 1) * (uint32_t)(ROW * 4);
+        s4m r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4m*)(uintptr_t)(b_addr[0] + bo));
+        s4m r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4m*)(uintptr_t)(b_addr[1] + bo));
+        s4m r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4m*)(uintptr_t)(b_addr[0] + bo + 2 * IMGH));
+        s4m r3 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4m*)(uintptr_t)(b_addr[1] + bo + 2 * IMGH));
+        typedef short s8m __attribute__((ext_vector_type(8)));
+        b_hi = __builtin_bit_cast(h8m, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+        b_lo = __builtin_bit_cast(h8m, __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7));
+        (void)sizeof(s8m);
+      } else {
+        const float* rowp = s_rows + (s & 1) * ROW + b_base;
 #pragma unroll
-      for (int st = 0; st < NK; ++st) b_op[st] = rowp[4 * st * PS];
+        for (int st = 0; st < NK; ++st) b_op[st] = rowp[4 * st * PS];
+      }
     }
     if (!guard || (s >= 1 && s - 1 >= 2 * R && s - 1 < nrows)) {
       // vertical pass of row s-1 over ring rows s-1-2R .. s-1 (slots j .. j+2R)
       bf2 v0 = bf2{0.f, 0.f}, v1 = bf2{0.f, 0.f}, u0 = bf2{0.f, 0.f}, u1 = bf2{0.f, 0.f};
+#ifdef MW_ABL_NOVERT
+      constexpr int NRV = 1;  // ablation: one vertical tap
+#else
+      constexpr int NRV = NR;
+#endif
 #pragma unroll
-      for (int i = 0; i < NR; ++i) {
+      for (int i = 0; i < NRV; ++i) {
         const f4m& rg = ring[(j + i) % NR];
-        const bf2 w2 = bf2{taps.w[i], taps.w[i]};
+        const bf2 w2 = bf2{taps.w[i], taps.w[i]};  // H16: x 2^-24 (launcher)
         if (i & 1) {
           v1 = __builtin_elementwise_fma(w2, bf2{rg.x, rg.y}, v1);
           u1 = __builtin_elementwise_fma(w2, bf2{rg.z, rg.w}, u1);
@@ -507,7 +611,9 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
       }
     }
     if constexpr (EPI == kEpiStore) {
+#ifndef MW_ABL_NOSTORE
       store_out(s & 1, y0 + s - 2 - 2 * R, !guard || s >= 2 + 2 * R);
+#endif
     } else if (!guard || s >= 2 + 2 * R) {
       // kept apart from the other stages: interleaved, the epilogue's
       // temporaries would lift the kernel past 128 VGPRs (one workgroup per CU)
@@ -517,13 +623,25 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
     }
     dma_row(s + LA);
     if (!guard || s < nrows) {
-      f4m d0 = f4m{0.f, 0.f, 0.f, 0.f}, d1 = f4m{0.f, 0.f, 0.f, 0.f};
+#ifdef MW_ABL_NOMFMA
+      if constexpr (H16) {  // ablation: no matrix-core work
+        ring[j] = __builtin_bit_cast(f4m, __builtin_shufflevector(b_hi, b_lo, 0, 1, 2, 3, 8, 9, 10, 11));
+      } else
+#endif
+      if constexpr (H16) {
+        // (hi + lo)(hi + lo) less lo*lo: three f16 products accumulated in fp32
+        f4m d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_hi, f4m{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_lo, b_hi, d, 0, 0, 0);
+        ring[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_lo, d, 0, 0, 0);
+      } else {
+        f4m d0 = f4m{0.f, 0.f, 0.f, 0.f}, d1 = f4m{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int st = 0; st < NK; st += 2) {
-        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a_op[st], b_op[st], d0, 0, 0, 0);
-        if (st + 1 < NK) d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a_op[st + 1], b_op[st + 1], d1, 0, 0, 0);
+        for (int st = 0; st < NK; st += 2) {
+          d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a_op[st], b_op[st], d0, 0, 0, 0);
+          if (st + 1 < NK) d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a_op[st + 1], b_op[st + 1], d1, 0, 0, 0);
+        }
+        ring[j] = d0 + d1;
       }
-      ring[j] = d0 + d1;
     }
     if (full) {
       if (guard && s < LA - 2) vm_wait_n<(LA - 2) * NG + kStore>();  // prologue DMAs, no stores yet
@@ -556,30 +674,30 @@ __global__ void __launch_bounds__(64 * BT * CT, EPI == kEpiStore ? 1 : 4) blur_m
   vm_wait_n<0>();  // no DMA may still target this workgroup's LDS at exit
 }
 
+template <typename T, int R, int CT, int BT, int EPI, bool LOGN>
+static int launch_blur_mfma_one(const T* in, int H, int W, int C, const float* inv_mean, float p,
+                                const BlurTaps& taps, float* out, const BlurEpi& ep, hipStream_t st) {
+  using K = BlurMfmaCfg<T, R, CT, BT, EPI, LOGN && kBlurH16>;  // as the kernel instance
+  const size_t lds = K::lds_bytes();
+  if (lds > 160 * 1024 || K::D < 4) return MW_EUNSUPPORTED;
+  const int nbx = (W + K::BW - 1) / K::BW;
+  const BlurGrid bg = blur_grid(H, nbx);
+  BlurTaps tv = taps;  // H16: the vertical taps carry the 2^-24 descale (exact)
+  if (LOGN && kBlurH16)
+    for (int i = 0; i <= 2 * R; ++i) tv.w[i] = taps.w[i] * kH16VS;
+  hipLaunchKernelGGL((blur_mfma_kernel<T, R, CT, BT, LOGN, EPI>), dim3(bg.ntiles), dim3(K::NT), lds, st, in, H,
+                     W, C, inv_mean, p, tv, out, ep, bg);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
 template <typename T, int R, int CT, int BT, int EPI>
 static int launch_blur_mfma_rc(const T* in, int H, int W, int C, const float* inv_mean, float p,
                                const BlurTaps& taps, float* out, const BlurEpi& ep, hipStream_t st) {
-  using K = BlurMfmaCfg<T, R, CT, BT, EPI>;
-  {
-    const size_t lds = K::lds_bytes();
-    if (lds > 160 * 1024 || K::D < 4) return MW_EUNSUPPORTED;
-    const int nbx = (W + K::BW - 1) / K::BW;
-    if (inv_mean) {
-      auto kern = blur_mfma_kernel<T, R, CT, BT, true, EPI>;
-      const BlurGrid bg = blur_grid(H, nbx);
-      hipLaunchKernelGGL(kern, dim3(bg.ntiles), dim3(K::NT), lds, st, in, H, W, C, inv_mean, p, taps, out,
-                         ep, bg);
-    } else if constexpr (EPI == kEpiStore) {
-      auto kern = blur_mfma_kernel<T, R, CT, BT, false, EPI>;
-      const BlurGrid bg = blur_grid(H, nbx);
-      hipLaunchKernelGGL(kern, dim3(bg.ntiles), dim3(K::NT), lds, st, in, H, W, C, inv_mean, p, taps, out,
-                         ep, bg);
-    } else {
-      return MW_EUNSUPPORTED;  // the fused epilogues follow a log-normalise
-    }
-    MW_LAUNCH_CHECK();
-    return MW_OK;
-  }
+  if (inv_mean) return launch_blur_mfma_one<T, R, CT, BT, EPI, true>(in, H, W, C, inv_mean, p, taps, out, ep, st);
+  if constexpr (EPI == kEpiStore)
+    return launch_blur_mfma_one<T, R, CT, BT, EPI, false>(in, H, W, C, inv_mean, p, taps, out, ep, st);
+  return MW_EUNSUPPORTED;  // the fused epilogues follow a log-normalise
 }
 
 template <typename T, int R>

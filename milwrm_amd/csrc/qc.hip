@@ -13,10 +13,13 @@
 // reference (`tissue_ID == i` is false for NaN).  Domains d0 .. d0+k-1 per
 // launch (label l counts as domain l - d0): more domains take more launches.
 //
-// Exact sums: every fp64 term (the squared error, y, y^2) is rounded once to
-// a per-feature fixed point, q = rint(v * 2^e) with |q| <= 2^38 (the host
-// derives e from the column max |x| of the slide, its scaler and the
-// centers), and summed as int64.  Integer sums do not depend on order, so the
+// Exact sums: every fp64 term (the squared error, y, y^2) is rounded to a
+// per-feature two-level fixed point, q = rint(v * 2^e) with |q| <= 2^38 (the
+// host derives e from the column max |x| of the slide, its scaler and the
+// centers) plus the residual's own 38 bits, r = rint((v * 2^e - q) * 2^38), and
+// both are summed as int64: a term far below the column bound (the squared
+// error of a domain packed around its center) keeps ~2^-76 of the bound, not
+// 2^-38 — fp64-grade relative accuracy.  Integer sums do not depend on order, so the
 // statistics are the same bits for any split of the pixels: a slide blurred
 // band by band into a reused buffer (the deferred-blur mode, no full fp32
 // copy) gives exactly the materialised slide's numbers, and so would pixels
@@ -36,11 +39,17 @@
 namespace mw {
 
 constexpr int kQcThreads = 256;
-constexpr int kQcMaxK = 20;  // LDS <= 20*256*8 + 2*256*8 + 20*256*4 (F = 1) = 64 KiB, the default limit
+constexpr int kQcMaxK = 20;  // LDS <= 2*20*256*8 + 4*256*8 + 20*256*4 (F = 1) = 108 KiB
 constexpr int kQcMaxBlocks = 2048;
 constexpr int kQcUnroll = 8;
 
-__device__ __forceinline__ long long qc_fix(double v, int e) { return (long long)rint(ldexp(v, e)); }
+// two-level fixed point of v at exponent e: hi += rint(v 2^e), lo += rint(residual 2^38)
+__device__ __forceinline__ void qc_fix2(double v, int e, long long& hi, long long& lo) {
+  const double s = ldexp(v, e);
+  const double h = rint(s);
+  hi += (long long)h;
+  lo += (long long)rint(ldexp(s - h, 38));  // s - h exact (|s| < 2^39)
+}
 
 __device__ __forceinline__ void qc_limbs(long long v, double& hi, double& lo) {
   const long long h = v >> 32;  // arithmetic shift: floor
@@ -48,44 +57,48 @@ __device__ __forceinline__ void qc_limbs(long long v, double& hi, double& lo) {
   lo = (double)(v - h * (1LL << 32));
 }
 
+template <typename TI>
 __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
-    const float* __restrict__ img, int C, const int32_t* __restrict__ feat, int F,
+    const TI* __restrict__ img, int C, const int32_t* __restrict__ feat, int F,
     const double* __restrict__ a, const double* __restrict__ b, const double* __restrict__ pivot,
     const double* __restrict__ centers, const int32_t* __restrict__ qe, int k, int d0,
     const int8_t* __restrict__ label, int64_t n_pix, int M, double* __restrict__ part) {
   extern __shared__ long long lds[];
-  long long* sse = lds;                                        // [k][256]
-  long long* s1s = sse + (size_t)k * kQcThreads;               // [256]
-  long long* s2s = s1s + kQcThreads;                           // [256]
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(s2s + kQcThreads);  // [k][groups]
+  long long* sse = lds;                                        // [2][k][256] (hi, lo)
+  long long* sacc = sse + 2 * (size_t)k * kQcThreads;          // [4][256]: s1 hi, lo, s2 hi, lo
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(sacc + 4 * kQcThreads);  // [k][groups]
+  const size_t KL = (size_t)k * kQcThreads;                    // lo offset
   const int t = threadIdx.x;
   const int groups = kQcThreads / F;
   const int g = t / F, f = t - g * F;
-  for (int d = 0; d < k; ++d) sse[d * kQcThreads + t] = 0;
+  for (int d = 0; d < 2 * k; ++d) sse[d * kQcThreads + t] = 0;
   for (int i = t; i < k * groups; i += kQcThreads) cnt[i] = 0u;
   __syncthreads();
-  long long s1 = 0, s2 = 0;
+  long long s1 = 0, s1l = 0, s2 = 0, s2l = 0;
   if (g < groups) {
     const int ch = feat[f];
     const double af = a[f], bf = b[f], pf = pivot[f];
     const int es = qe[f], e1 = qe[F + f], e2 = qe[2 * F + f];
     const int64_t step = (int64_t)gridDim.x * groups;
-    auto add = [&](float v, int l) {
+    auto add = [&](TI v, int l) {
       const double x = (double)v * af + bf;
       const double y = x - pf;
-      s1 += qc_fix(y, e1);
-      s2 += qc_fix(y * y, e2);
+      qc_fix2(y, e1, s1, s1l);
+      qc_fix2(y * y, e2, s2, s2l);
       l -= d0;
       if (l >= 0 && l < k) {
         const double dd = x - centers[l * F + f];
-        sse[l * kQcThreads + t] += qc_fix(dd * dd, es);
+        long long h = 0, lo = 0;
+        qc_fix2(dd * dd, es, h, lo);
+        sse[l * kQcThreads + t] += h;
+        sse[KL + l * kQcThreads + t] += lo;
         if (f == 0) cnt[l * groups + g] += 1u;
       }
     };
     int64_t p = (int64_t)blockIdx.x * groups + g;
     // kQcUnroll pixels' loads in flight before their (LDS read-modify-write) updates
     for (; p + (kQcUnroll - 1) * step < n_pix; p += kQcUnroll * step) {
-      float v[kQcUnroll];
+      TI v[kQcUnroll];
       int l[kQcUnroll];
 #pragma unroll
       for (int u = 0; u < kQcUnroll; ++u) {
@@ -97,34 +110,37 @@ __global__ __launch_bounds__(kQcThreads) void domain_sse_kernel(
     }
     for (; p < n_pix; p += step) add(img[p * C + ch], label[p]);
   }
-  s1s[t] = s1;
-  s2s[t] = s2;
+  sacc[t] = s1;
+  sacc[kQcThreads + t] = s1l;
+  sacc[2 * kQcThreads + t] = s2;
+  sacc[3 * kQcThreads + t] = s2l;
   __syncthreads();
-  // fold the groups (int64, exact) and emit limbs:
-  // [sse k*F | sum F | sumsq F] as (hi, lo) pairs, then count k
+  // fold the groups (int64, exact) and emit limbs: quantities
+  // [sse k*F | sum F | sumsq F], each level (hi sums, then lo sums) as
+  // (upper, lower) 32-bit limbs, then count k:
+  //   [L0 upper NQ | L0 lower NQ | L1 upper NQ | L1 lower NQ | count k]
   const int NQ = k * F + 2 * F;
-  for (int e = t; e < NQ + k; e += kQcThreads) {
-    if (e < NQ) {
+  for (int e = t; e < 2 * NQ + k; e += kQcThreads) {
+    if (e < 2 * NQ) {
+      const int lv = e >= NQ, qi = e - lv * NQ;
       long long r = 0;
-      if (e < k * F) {
-        const int d = e / F, ff = e - d * F;
-        for (int gg = 0; gg < groups; ++gg) r += sse[d * kQcThreads + gg * F + ff];
-      } else if (e < k * F + F) {
-        const int ff = e - k * F;
-        for (int gg = 0; gg < groups; ++gg) r += s1s[gg * F + ff];
+      if (qi < k * F) {
+        const int d = qi / F, ff = qi - d * F;
+        for (int gg = 0; gg < groups; ++gg) r += sse[lv * KL + d * kQcThreads + gg * F + ff];
       } else {
-        const int ff = e - k * F - F;
-        for (int gg = 0; gg < groups; ++gg) r += s2s[gg * F + ff];
+        const int which = qi < k * F + F ? 0 : 1, ff = qi - k * F - which * F;
+        const long long* sa = sacc + (2 * which + lv) * kQcThreads;
+        for (int gg = 0; gg < groups; ++gg) r += sa[gg * F + ff];
       }
       double hi, lo;
       qc_limbs(r, hi, lo);
-      part[(size_t)blockIdx.x * M + e] = hi;
-      part[(size_t)blockIdx.x * M + NQ + e] = lo;
+      part[(size_t)blockIdx.x * M + 2 * lv * NQ + qi] = hi;
+      part[(size_t)blockIdx.x * M + (2 * lv + 1) * NQ + qi] = lo;
     } else {
-      const int d = e - NQ;
+      const int d = e - 2 * NQ;
       double r = 0.0;
       for (int gg = 0; gg < groups; ++gg) r += (double)cnt[d * groups + gg];
-      part[(size_t)blockIdx.x * M + 2 * NQ + d] = r;
+      part[(size_t)blockIdx.x * M + 4 * NQ + d] = r;
     }
   }
 }
@@ -154,7 +170,7 @@ using namespace mw;
 
 extern "C" {
 
-int mw_domain_sse_out_len(int k, int F) { return 2 * (k * F + 2 * F) + k; }
+int mw_domain_sse_out_len(int k, int F) { return 4 * (k * F + 2 * F) + k; }
 
 size_t mw_domain_sse_ws_bytes(int64_t n_pix, int k, int F) {
   if (n_pix <= 0 || k <= 0 || F <= 0 || F > kQcThreads) return 0;
@@ -167,10 +183,13 @@ static int64_t qc_pixels_per_block(int64_t n_pix, int F) {
   return (n_pix + G - 1) / G;
 }
 
-int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
-                  const double* d_b, const double* d_pivot, const double* d_centers,
-                  const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
-                  double* d_out, int accumulate, void* d_ws, void* stream) {
+}  // extern "C"
+
+template <typename TI>
+static int domain_sse_launch(const TI* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
+                             const double* d_b, const double* d_pivot, const double* d_centers,
+                             const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
+                             double* d_out, int accumulate, void* d_ws, void* stream) {
   MW_CHECK_ARG(d_img && d_feat && d_a && d_b && d_pivot && d_centers && d_qexp && d_label && d_out && d_ws,
                "mw_domain_sse: null pointer");
   MW_CHECK_ARG(n_pix > 0 && C > 0 && F > 0 && F <= kQcThreads && k >= 1 && k <= kQcMaxK && d0 >= 0,
@@ -182,15 +201,33 @@ int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const
   hipStream_t st = as_stream(stream);
   const int G = qc_blocks(n_pix, F);
   const int M = mw_domain_sse_out_len(k, F);
-  const size_t lds = (size_t)k * kQcThreads * sizeof(long long) + 2 * kQcThreads * sizeof(long long) +
+  const size_t lds = 2 * (size_t)k * kQcThreads * sizeof(long long) + 4 * kQcThreads * sizeof(long long) +
                      (size_t)k * (kQcThreads / F) * sizeof(uint32_t);
   double* part = reinterpret_cast<double*>(d_ws);
-  hipLaunchKernelGGL(domain_sse_kernel, dim3(G), dim3(kQcThreads), lds, st, d_img, C, d_feat, F,
+  hipLaunchKernelGGL(domain_sse_kernel<TI>, dim3(G), dim3(kQcThreads), lds, st, d_img, C, d_feat, F,
                      d_a, d_b, d_pivot, d_centers, d_qexp, k, d0, d_label, n_pix, M, part);
   MW_LAUNCH_CHECK();
   hipLaunchKernelGGL(domain_sse_reduce, dim3(M), dim3(256), 0, st, part, G, M, accumulate, d_out);
   MW_LAUNCH_CHECK();
   return MW_OK;
+}
+
+extern "C" {
+
+int mw_domain_sse(const float* d_img, int C, const int32_t* d_feat, int F, const double* d_a,
+                  const double* d_b, const double* d_pivot, const double* d_centers,
+                  const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
+                  double* d_out, int accumulate, void* d_ws, void* stream) {
+  return domain_sse_launch<float>(d_img, C, d_feat, F, d_a, d_b, d_pivot, d_centers, d_qexp, k, d0, d_label,
+                                  n_pix, d_out, accumulate, d_ws, stream);
+}
+
+int mw_domain_sse_f64(const double* d_rows, int C, const int32_t* d_feat, int F, const double* d_a,
+                      const double* d_b, const double* d_pivot, const double* d_centers,
+                      const int32_t* d_qexp, int k, int d0, const int8_t* d_label, int64_t n_pix,
+                      double* d_out, int accumulate, void* d_ws, void* stream) {
+  return domain_sse_launch<double>(d_rows, C, d_feat, F, d_a, d_b, d_pivot, d_centers, d_qexp, k, d0, d_label,
+                                   n_pix, d_out, accumulate, d_ws, stream);
 }
 
 }  // extern "C"
