@@ -535,14 +535,17 @@ class mxif_labeler(tissue_labeler):
             self.image_df["Img"] = paths
         else:
             self._images = images
-        for tot, S in totals:
-            check_total(tot, S)
-        set_global_state_after_draws()  # np.random as the reference leaves it (MxIF.py:484-490)
-        st = comm.merge_image_stats(D.d2h(img_stats), F)
+        # np.random as the reference leaves it (MxIF.py:484-490): waits for the
+        # last draw's counts only, so the host replay overlaps the gather
+        set_global_state_after_draws()
+        host = D.d2h(img_stats, xmax, *[t for t, _ in totals])  # one synchronisation
+        for (_, S), tot in zip(totals, host[2:]):
+            check_total(int(tot[0]), S)
+        st = comm.merge_image_stats(host[0], F)
         self.scaler = StandardScaler.from_stats(st)
         mu, inv = self.scaler.affine()
         self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv,
-                                xmax_local=D.d2h(xmax))
+                                xmax_local=host[1])
         self._cluster_host = None
 
     def _image_list(self):

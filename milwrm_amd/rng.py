@@ -67,7 +67,7 @@ def subsample_indices_device(M: int, fract: float, random_state: int = 16, devic
 
     dev = device if device is not None else D.device()
     S = int(M * fract)
-    _LAST_DRAW.clear()
+    _release_last_draw()
     out = torch.empty(S, dtype=torch.int32, device=dev)
     total = torch.zeros(1, dtype=torch.int64, device=dev)
     if S == 0:
@@ -80,11 +80,30 @@ def subsample_indices_device(M: int, fract: float, random_state: int = 16, devic
     ws = D.WS.get("mtrng", N.query("mw_legacy_randint_gen_ws_bytes", int(M), S, MT_SEGMENT))
     N.call("mw_legacy_randint_from_states", D.P(states), W_avail, int(M), S, MT_SEGMENT, D.P(out),
            D.P(total), D.P(ws), D.stream())
-    _LAST_DRAW.update(M=int(M), S=S, seed=seed, W=int(W), ws=ws, states=states)
+    # the per-segment accepted counts go to the host behind an event of their
+    # own, so set_global_state_after_draws waits for them, not for the kernels
+    # queued after the draw (the host replay then overlaps the gather)
+    cnt = ws[int(W) * MT_SEGMENT * 4:int(W) * MT_SEGMENT * 4 + int(W) * 8].view(torch.int64)
+    slot = D._PINNED.take(int(W) * 8)  # pooled page-locked buffer, held until the replay
+    slot[1] = D._Busy
+    cnt_host = slot[0][:int(W) * 8].view(torch.int64)
+    cnt_host.copy_(cnt, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    _LAST_DRAW.update(M=int(M), S=S, seed=seed, W=int(W), cnt_host=cnt_host, ev=ev, slot=slot,
+                      states_key=(str(dev), seed))
     return out, total
 
 
 _LAST_DRAW = {}  # the newest device draw: what the global NumPy state must be advanced past
+
+
+def _release_last_draw():
+    slot = _LAST_DRAW.get("slot")
+    if slot is not None:
+        _LAST_DRAW["ev"].synchronize()  # the copy into the slot has landed
+        slot[1] = None
+    _LAST_DRAW.clear()
 
 
 def set_global_state_after_draws() -> None:
@@ -102,15 +121,16 @@ def set_global_state_after_draws() -> None:
     from . import device as D
 
     last = dict(_LAST_DRAW)
-    _LAST_DRAW.clear()
     if not last or last["S"] == 0 or last["M"] < 2:
+        _release_last_draw()
         return
-    W, L, S = last["W"], MT_SEGMENT, last["S"]
-    cnt = last["ws"][W * L * 4:W * L * 4 + W * 8].view(torch.int64)
-    off = D.d2h(cnt)
+    L, S = MT_SEGMENT, last["S"]
+    last["ev"].synchronize()
+    off = last["cnt_host"].numpy().copy()
+    _release_last_draw()
     w = int(np.searchsorted(off, S - 1, side="right")) - 1
     need = S - int(off[w])  # accepted draws still needed inside segment w
-    key = D.d2h(last["states"][w * 624:(w + 1) * 624]).view(np.uint32)
+    key = _segment_states_host(last["states_key"])[w * 624:(w + 1) * 624].view(np.uint32)
     r = np.uint64(last["M"] - 1)
     m = r
     for s in (1, 2, 4, 8, 16):
@@ -154,8 +174,25 @@ def _segment_states(dev, seed: int, W: int):
     return _states[key]
 
 
+_states_host = {}
+
+
+def _segment_states_host(key):
+    """Host copy of the memoised segment start states (copied once per
+    (device, seed, size): they never change once built)."""
+    from . import device as D
+
+    states, W = _states[key]
+    hit = _states_host.get(key)
+    if hit is None or hit[1] != W:
+        hit = (D.d2h(states), W)
+        _states_host[key] = hit
+    return hit[0]
+
+
 def check_total(total, S: int):
-    if S and int(total.item()) < S:  # pragma: no cover - 16-sigma margin
+    """``total``: the device count (one sync) or its host value."""
+    if S and int(total.item() if hasattr(total, "item") else total) < S:  # pragma: no cover - 16-sigma margin
         raise RuntimeError("device MT19937 produced too few accepted draws; increase the margin")
 
 

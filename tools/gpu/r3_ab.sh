@@ -12,6 +12,11 @@ if [ -n "$LIBS" ]; then
   timeout -k 10 400 env LIBS="$LIBS" SIZE="${SIZE:-10000}" CH="${CH:-30}" bash tools/dev/blur_ab.sh > gpurun_out/ab/blur_ab.log 2>&1
   rc=$?; cat gpurun_out/ab/blur_ab.log | grep -v "^$" | tail -12; fatal $rc && exit $rc
 fi
+if [ -n "$BH" ]; then
+  echo "[gpu] blur band-height sweep: $BH"
+  timeout -k 10 300 python tools/blur_bench.py ${SIZE:-10000} ${CH:-30} "$BH" > gpurun_out/ab/bh.log 2>&1
+  rc=$?; grep "BW=" gpurun_out/ab/bh.log; fatal $rc && exit $rc
+fi
 if [ -n "$TESTS" ]; then
   echo "[gpu] pytest -m gpu $TESTS"
   timeout -k 10 600 python -u -m pytest $TESTS -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/ab/pytest.log 2>&1
