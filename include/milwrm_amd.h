@@ -110,24 +110,26 @@ int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stre
 /* ---- fused blur + subsample (MxIF.py:375-394 + 457-492, MILWRM.py:1716-1733)
  * The subsample rows are written by the blur itself, so the blurred slide is
  * never stored:
- *   mw_sample_map:   head[p] = smallest j with rank2pix[idx[j]] == p (INT32 max
- *                    if none; d_head holds mw_sample_head_elems(n_pix) int32),
- *                    pix[j] = rank2pix[idx[j]];
- *   mw_blur_sample:  lognorm + blur of the slide; X[head[p], f] =
- *                    blurred[p, feat[f]] for every sampled pixel p;
- *   mw_sample_fixup: X[j] = X[head[pix[j]]] for the repeated draws;
+ *   mw_sample_map:      slots[2p], slots[2p+1] = the first two sample slots j
+ *                       of pixel p (rank2pix[idx[j]] == p; -1 where absent;
+ *                       d_slots holds mw_sample_slot_elems(n_pix) int32), the
+ *                       later slots of p on the overflow list d_ovf (S + 1
+ *                       int32: [0] = count, then the slots);
+ *   mw_blur_sample:     lognorm + blur of the slide; X[j, f] = blurred[p,
+ *                       feat[f]] for both table slots j of every sampled p;
+ *   mw_sample_overflow: X[j] = X[slots[2p]] for the overflow slots;
  * then mw_col_stats_rows.  X ends up equal to mw_blur + mw_gather_rows.
  * mw_blur_sample returns MW_EUNSUPPORTED (nothing launched) for shapes the
  * fused kernel does not take (odd C, C > 64, radius 0 or > 8, F > C rounded
  * up to 16, no log-normalise); the caller then materialises the blur. */
-size_t mw_sample_head_elems(int64_t n_pix);
+size_t mw_sample_slot_elems(int64_t n_pix);
 int mw_sample_map(const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S, int64_t n_pix,
-                  int32_t* d_head, int32_t* d_pix, void* stream);
+                  int32_t* d_slots, int32_t* d_ovf, void* stream);
 int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
-                   float pseudoval, const float* h_weights, int radius, const int32_t* d_head,
+                   float pseudoval, const float* h_weights, int radius, const int32_t* d_slots,
                    int64_t S, const int32_t* d_feat, int F, float* d_X, void* stream);
-int mw_sample_fixup(const int32_t* d_pix, const int32_t* d_head, int64_t S, int F, float* d_X,
-                    void* stream);
+int mw_sample_overflow(const int32_t* d_idx, const uint32_t* d_rank2pix, const int32_t* d_slots,
+                       const int32_t* d_ovf, int64_t S, int F, float* d_X, void* stream);
 
 /* Chan-merge the per-block stats of the last gather(s) into d_stats =
  * [n, mean[F], M2[F]] (fp64).  `n_parts` gathers may be accumulated: pass

@@ -81,10 +81,10 @@ _PROTOS = {
     "mw_neighbor_mean": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_col_stats_rows": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_col_stats_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),
-    "mw_sample_head_elems": (c_sz, [c_i64]),
+    "mw_sample_slot_elems": (c_sz, [c_i64]),
     "mw_sample_map": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mw_blur_sample": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
-    "mw_sample_fixup": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mw_sample_overflow": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_blur_assign_conf": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mw_domain_records": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mw_synth_slide": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_u64, c_vp, c_vp, c_vp]),

@@ -39,10 +39,10 @@ template <typename T>
 int launch_blur_fast(const T* in, int H, int W, int C, const float* inv_mean, float p,
                      const struct BlurTaps& taps, int r, float* out, hipStream_t st);
 constexpr int kEpiStore = 0, kEpiSample = 1, kEpiAssign = 2;
-constexpr int kEpiKS = 16;  // assign epilogue: center stride (k <= 2 * threads per column)
+constexpr int kEpiKMax = 16;  // assign epilogue: centers per launch (distance tables in LDS)
 
 struct BlurEpi {
-  const int32_t* head;     // kEpiSample: n_pix + 128 slots (int32 max: no sample)
+  const int32_t* slots;    // kEpiSample: (n_pix + 128) x 2: the first two sample slots of p (-1: none)
   int64_t S;               //   rows of X
   float* X;                //   S x F
   int F;

@@ -146,7 +146,10 @@ struct BlurMfmaCfg {
   static constexpr int SLOT = NPIECE * 1024;    // bytes per raw ring slot
   static constexpr int NCH = (SLOT / 16 + NT - 1) / NT;  // 16-byte chunks per thread
   static constexpr int NP = NCH * Chunk16<T>::P;  // element pairs per thread
-  static constexpr size_t EXTRA = EPI == kEpiAssign ? (size_t)8 * CT * kEpiKS * 8 : 0;  // centers
+  // kEpiAssign: per output row the k distances of its BW pixels and their
+  // mask bytes, double-buffered (written one step, reduced the next)
+  static constexpr size_t EXTRA =
+      EPI == kEpiAssign ? 2 * ((size_t)kEpiKMax * BW * 4 + BW) + (size_t)kEpiKMax * 8 * CT * 8 : 0;
   static constexpr size_t FIXED = (2 * (size_t)ROW + 2 * (size_t)STG) * sizeof(float) + 64 + EXTRA;
   static constexpr int AUXOFF = NPC * 1024;     // side-data piece
   static constexpr int AUXW = NPC % NW;
@@ -227,7 +230,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
                                                                  BlurGrid bg) {
   constexpr bool H16 = LOGN && kBlurH16;
   using K = BlurMfmaCfg<T, R, CT, BT, EPI, H16>;
-  constexpr int NS = K::NS, KS = kEpiKS;
+  constexpr int NS = K::NS;
   constexpr int U = K::U, IMGH = K::IMGH, NPXS = K::NPXS;
   constexpr int NR = K::NR, BW = K::BW, NPX = K::NPX, PS = K::PS, NK = K::NK, NT = K::NT;
   constexpr int ROW = K::ROW, STG = K::STG, NCH = K::NCH, NP = K::NP, CP = Chunk16<T>::P;
@@ -247,7 +250,9 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
   float* s_stg = smem + 2 * ROW;              // 2 x STG  (output staging rows, HWC)
   float* s_dummy = smem + 2 * ROW + 2 * STG;  // 64 bytes: sink of pad pairs
   char* s_raw = reinterpret_cast<char*>(smem) + K::FIXED;  // D x SLOT raw input rows
-  f2m_* s_cT = reinterpret_cast<f2m_*>(s_dummy + 16);      // kEpiAssign: centers [pair][KS]
+  float* s_dist = s_dummy + 16;                            // kEpiAssign: [2][k][BW] distances
+  uint8_t* s_mk = reinterpret_cast<uint8_t*>(s_dist + 2 * kEpiKMax * BW);  // [2][BW] mask bytes
+  f2m_* s_cen = reinterpret_cast<f2m_*>(s_mk + 2 * BW);   // [k][8 CT] center pairs
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -354,13 +359,13 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
       fo[i][0] = f0 < ep.F ? ep.feat[f0] : -1;
       fo[i][1] = f0 + 1 < ep.F ? ep.feat[f0 + 1] : -1;
     }
-    aux_off = (uint32_t)lane * 16u < (uint32_t)(BW + 4) * 4u ? (uint32_t)lane * 16u : 0u;
+    aux_off = (uint32_t)lane * 16u < (uint32_t)(BW + 2) * 8u ? (uint32_t)lane * 16u : 0u;
   }
   if constexpr (EPI == kEpiAssign) {
-    for (int q = t; q < 8 * CT * KS; q += NT) {
-      const int p = q / KS, j = q - p * KS;
-      const bool ok = j < ep.k && 2 * p < C;  // C even (launcher)
-      s_cT[q] = ok ? f2m_{ep.centers[j * C + 2 * p], ep.centers[j * C + 2 * p + 1]} : f2m_{0.f, 0.f};
+    for (int q = t; q < kEpiKMax * 8 * CT; q += NT) {
+      const int j = q / (8 * CT), p2 = q - j * (8 * CT);
+      const bool ok = j < ep.k && 2 * p2 < C;  // C even (launcher)
+      s_cen[q] = ok ? f2m_{ep.centers[j * C + 2 * p2], ep.centers[j * C + 2 * p2 + 1]} : f2m_{0.f, 0.f};
     }
     if (st_ok) {
       sc_a = ep.a[16 * ct + m];
@@ -390,7 +395,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
           yq = yq < y0 ? y0 : (yq >= y1 ? y1 - 1 : yq);
           const int64_t rp = (int64_t)yq * W + x0;
           const char* asrc = EPI == kEpiSample
-                                 ? reinterpret_cast<const char*>(ep.head) + ((rp * 4) & ~(int64_t)15)
+                                 ? reinterpret_cast<const char*>(ep.slots) + ((rp * 8) & ~(int64_t)15)
                                  : reinterpret_cast<const char*>(ep.mask) + (rp & ~(int64_t)15);
           glds16(asrc, aux_off, slot + (uint32_t)(g * NT + 64 * wv) * 16u);
           continue;
@@ -479,63 +484,73 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
     const char* auxp = s_raw + (s % D) * SLOT + K::AUXOFF;
     const float* srow = s_stg + (s & 1) * STG + ecol * C;
     if constexpr (EPI == kEpiSample) {
-      const int h = reinterpret_cast<const int*>(auxp)[(int)(rowpix & 3) + ecol];
-      if (ecol < bw && (uint64_t)(uint32_t)h < (uint64_t)ep.S) {
-        float* dst = ep.X + (int64_t)h * ep.F;
+      // the pixel's first two sample slots (mw_sample_map; -1: none): this
+      // thread's features from the staged row, one store per slot
+      const int2 sl = reinterpret_cast<const int2*>(auxp)[(int)(rowpix & 1) + ecol];
+      if (ecol < bw && (uint64_t)(uint32_t)sl.x < (uint64_t)ep.S) {
+        const bool dup = (uint64_t)(uint32_t)sl.y < (uint64_t)ep.S;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int f0 = 2 * (esub + NS * i);
           if (fo[i][0] < 0) continue;
-          const float v0 = srow[fo[i][0]];
-          if (fo[i][1] >= 0 && (ep.F & 1) == 0) {
-            *reinterpret_cast<f2m_*>(dst + f0) = f2m_{v0, srow[fo[i][1]]};
-          } else {
-            dst[f0] = v0;
-            if (fo[i][1] >= 0) dst[f0 + 1] = srow[fo[i][1]];
+          const bool two = fo[i][1] >= 0;
+          const f2m_ v = f2m_{srow[fo[i][0]], two ? srow[fo[i][1]] : 0.f};
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            if (u == 1 && !dup) break;
+            float* dst = ep.X + (int64_t)(u ? sl.y : sl.x) * ep.F;
+            if (two && (ep.F & 1) == 0) {
+              *reinterpret_cast<f2m_*>(dst + f0) = v;
+            } else {
+              dst[f0] = v.x;
+              if (two) dst[f0 + 1] = v.y;
+            }
           }
         }
       }
     } else {
-      // distances of this column's pixel to centers esub and esub + NS: the
-      // Lloyd/assign E-step chain (even features in .x, odd in .y, pair order)
-      const uint8_t mk = reinterpret_cast<const uint8_t*>(auxp)[(int)(rowpix & 15) + ecol];
-      const f2m_* xp = reinterpret_cast<const f2m_*>(srow);
-      const f2m_* cp = s_cT + esub;
+      // distance phase: wave w takes centers w, w + NW, ... (wave-uniform:
+      // the center comes by scalar loads), lane = pixel column of the staged
+      // row; the Lloyd/assign E-step chain (even features in .x, odd in .y,
+      // pair order, then .x + .y), so the distances are the assign kernel's
+      // bits.  The argmin over the k tables runs next step (argmin_phase).
       const int np = C >> 1;
-      f2m_ acc0 = f2m_{0.f, 0.f}, acc1 = f2m_{0.f, 0.f};
-      if (ep.k > NS) {
-        for (int p = 0; p < np; ++p) {
-          const f2m_ x = xp[p];
-          const f2m_ d0 = x - cp[p * KS], d1 = x - cp[p * KS + NS];
-          acc0 = __builtin_elementwise_fma(d0, d0, acc0);
-          acc1 = __builtin_elementwise_fma(d1, d1, acc1);
+      const f2m_* xp = reinterpret_cast<const f2m_*>(s_stg + (s & 1) * STG + lane * C);
+      float* dst = s_dist + (s & 1) * kEpiKMax * BW;
+      for (int c0 = wv; c0 < ep.k; c0 += K::NW) {
+        const f2m_* cj = s_cen + c0 * (8 * CT);  // wave-uniform address: broadcast reads
+        f2m_ acc = f2m_{0.f, 0.f};
+#pragma unroll 4
+        for (int p2 = 0; p2 < np; ++p2) {
+          const f2m_ d = xp[p2] - cj[p2];
+          acc = __builtin_elementwise_fma(d, d, acc);
         }
-      } else {
-        for (int p = 0; p < np; ++p) {
-          const f2m_ d0 = xp[p] - cp[p * KS];
-          acc0 = __builtin_elementwise_fma(d0, d0, acc0);
-        }
+        dst[c0 * BW + lane] = acc.x + acc.y;
       }
-      const float dd0 = acc0.x + acc0.y, dd1 = acc1.x + acc1.y;
-      // strict argmin in center order + second smallest (nearest_centers<TOP2>)
-      const int lb = lane & ~(NS - 1);
-      int lab = 0;
-      float m1 = 0.f, m2 = __builtin_inff();
-      for (int j = 0; j < ep.k; ++j) {
-        const float dd = __shfl(j < NS ? dd0 : dd1, lb + (j & (NS - 1)), 64);
-        if (j == 0) { m1 = dd; lab = 0; }
-        else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
-        else if (dd < m2) { m2 = dd; }
-      }
-      const bool in_mask = ecol < bw && mk != 0;
-      const float conf = in_mask ? (m2 - m1) / m2 : __builtin_nanf("");
-      if (!in_mask) lab = -1;
-      if (esub == 0 && ecol < bw) {
-        ep.lab[rowpix + ecol] = (int8_t)lab;
-        ep.conf[rowpix + ecol] = conf;
-      }
+      if (wv == K::NW - 1 && lane < BW)  // the row's mask bytes travel with its distances
+        s_mk[(s & 1) * BW + lane] = reinterpret_cast<const uint8_t*>(auxp)[(int)(rowpix & 15) + lane];
     }
   };
+  // argmin phase for the row whose distances were written at step s - 1:
+  // strict argmin in center order + second smallest (nearest_centers<TOP2>),
+  // confidence (d2 - d1) / d2; one wave, lane = pixel column
+  auto argmin_phase = [&](int s) {
+    asm volatile("" : "+s"(s));
+    if (wv != (s % K::NW) || lane >= bw) return;
+    const int yo = y0 + (s - 1) - 2 - 2 * R;
+    const int64_t rowpix = (int64_t)yo * W + x0;
+    const float* dd = s_dist + ((s - 1) & 1) * kEpiKMax * BW + lane;
+    int lab = 0;
+    float m1 = dd[0], m2 = __builtin_inff();
+#pragma unroll 4
+    for (int j = 1; j < ep.k; ++j) {
+      const float d = dd[j * BW];
+      if (d < m1) { m2 = m1; m1 = d; lab = j; }
+      else if (d < m2) { m2 = d; }
+    }
+    const bool in_mask = s_mk[((s - 1) & 1) * BW + lane] != 0;
+    ep.lab[rowpix + lane] = (int8_t)(in_mask ? lab : -1);
+    ep.conf[rowpix + lane] = in_mask ? (m2 - m1) / m2 : __builtin_nanf("");  };
 
   lds_barrier();  // zero fill done
 #pragma unroll
@@ -619,6 +634,8 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
       // temporaries would lift the kernel past 128 VGPRs (one workgroup per CU)
       __builtin_amdgcn_sched_barrier(0);
       epilogue(s);
+      if constexpr (EPI == kEpiAssign)
+        if (!guard || s >= 3 + 2 * R) argmin_phase(s);
       __builtin_amdgcn_sched_barrier(0);
     }
     dma_row(s + LA);
@@ -671,6 +688,8 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
     for (int j = 0; j < NR; ++j)
       if (base + j < nsteps) step(base + j, j, true);
   }
+  if constexpr (EPI == kEpiAssign)  // the last row's argmin (its distances: the last step)
+    if (nsteps - 1 >= 2 + 2 * R) argmin_phase(nsteps);
   vm_wait_n<0>();  // no DMA may still target this workgroup's LDS at exit
 }
 
@@ -729,7 +748,7 @@ static int launch_blur_epi_rc(const T* in, int H, int W, int C, const float* inv
     if (ep.F > 16 * CT) return MW_EUNSUPPORTED;
     return launch_blur_mfma_rc<T, R, CT, 4, kEpiSample>(in, H, W, C, inv_mean, p, taps, nullptr, ep, st);
   }
-  if (ep.k > 2 * NS || ep.k > kEpiKS) return MW_EUNSUPPORTED;
+  if (ep.k < 1 || ep.k > kEpiKMax) return MW_EUNSUPPORTED;
   return launch_blur_mfma_rc<T, R, CT, 4, kEpiAssign>(in, H, W, C, inv_mean, p, taps, nullptr, ep, st);
 }
 template <typename T, int R>

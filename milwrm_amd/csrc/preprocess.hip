@@ -868,54 +868,63 @@ int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stre
 }
 
 // ------------------------------------------------- fused blur + subsample
-// head[p] = smallest sample slot j with rank2pix[idx[j]] == p (int32 max: p
-// not sampled), pix[j] = that pixel.  The blur's sample epilogue writes row
-// head[p] of X; sample_fixup copies it to the other slots of p (idx draws
-// with replacement).
+// Per sampled pixel p its first two sample slots (idx draws with replacement):
+// slots[p] = (j0, j1), -1 where absent; a third or later draw of p goes to the
+// overflow list ovf[1 + i] (ovf[0] = count; Poisson(0.2): ~0.6 % of the
+// sampled pixels).  The blur's sample epilogue writes rows j0 and j1 of X
+// (both read from the side data, no dependent load); mw_sample_overflow then
+// copies row j0 to the overflow slots.  Which draw lands in which place
+// depends on the atomic order, the rows written do not.
 __global__ void __launch_bounds__(256) sample_map_kernel(const int32_t* __restrict__ idx,
                                                          const uint32_t* __restrict__ r2p, int64_t S,
-                                                         int32_t* __restrict__ head,
-                                                         int32_t* __restrict__ pix) {
+                                                         int32_t* __restrict__ slots,
+                                                         int32_t* __restrict__ ovf) {
   for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < S; j += (int64_t)gridDim.x * 256) {
     const uint32_t p = r2p[idx[j]];
-    pix[j] = (int32_t)p;
-    atomicMin(head + p, (int32_t)j);
+    if (atomicCAS(slots + 2 * (int64_t)p, -1, (int32_t)j) == -1) continue;
+    if (atomicCAS(slots + 2 * (int64_t)p + 1, -1, (int32_t)j) == -1) continue;
+    ovf[1 + atomicAdd(ovf, 1)] = (int32_t)j;
   }
 }
-__global__ void __launch_bounds__(256) sample_fixup_kernel(const int32_t* __restrict__ pix,
-                                                           const int32_t* __restrict__ head, int64_t S,
-                                                           int F, float* __restrict__ X) {
-  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < S; j += (int64_t)gridDim.x * 256) {
-    const int32_t h = head[pix[j]];
-    if (h != (int32_t)j) {
-      const float* src = X + (int64_t)h * F;
-      float* dst = X + j * F;
-      for (int f = 0; f < F; ++f) dst[f] = src[f];
-    }
+__global__ void __launch_bounds__(256) sample_overflow_kernel(const int32_t* __restrict__ idx,
+                                                              const uint32_t* __restrict__ r2p,
+                                                              const int32_t* __restrict__ slots,
+                                                              const int32_t* __restrict__ ovf, int F,
+                                                              float* __restrict__ X) {
+  const int n = ovf[0];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int32_t j = ovf[1 + i];
+    const int32_t h = slots[2 * (int64_t)r2p[idx[j]]];
+    const float* src = X + (int64_t)h * F;
+    float* dst = X + (int64_t)j * F;
+    for (int f = 0; f < F; ++f) dst[f] = src[f];
   }
 }
 
-size_t mw_sample_head_elems(int64_t n_pix) { return (size_t)n_pix + 128; }
+size_t mw_sample_slot_elems(int64_t n_pix) { return 2 * ((size_t)n_pix + 128); }
 
 int mw_sample_map(const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S, int64_t n_pix,
-                  int32_t* d_head, int32_t* d_pix, void* stream) {
-  MW_CHECK_ARG(d_idx && d_rank2pix && d_head && d_pix, "mw_sample_map: null pointer");
+                  int32_t* d_slots, int32_t* d_ovf, void* stream) {
+  MW_CHECK_ARG(d_idx && d_rank2pix && d_slots && d_ovf, "mw_sample_map: null pointer");
   MW_CHECK_ARG(S > 0 && S < 0x7fffffffll && n_pix > 0, "mw_sample_map: bad sizes S=%lld n_pix=%lld",
                (long long)S, (long long)n_pix);
   hipStream_t st = as_stream(stream);
-  MW_HIP(hipMemsetAsync(d_head, 0x7f, mw_sample_head_elems(n_pix) * sizeof(int32_t), st));
+  MW_HIP(hipMemsetAsync(d_slots, 0xff, mw_sample_slot_elems(n_pix) * sizeof(int32_t), st));
+  MW_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), st));
   const int grid = (int)std::min<int64_t>((S + 255) / 256, 8192);
-  hipLaunchKernelGGL(sample_map_kernel, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, S, d_head, d_pix);
+  hipLaunchKernelGGL(sample_map_kernel, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, S, d_slots, d_ovf);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
 
-int mw_sample_fixup(const int32_t* d_pix, const int32_t* d_head, int64_t S, int F, float* d_X,
-                    void* stream) {
-  MW_CHECK_ARG(d_pix && d_head && d_X && S > 0 && F > 0, "mw_sample_fixup: bad args");
+int mw_sample_overflow(const int32_t* d_idx, const uint32_t* d_rank2pix, const int32_t* d_slots,
+                       const int32_t* d_ovf, int64_t S, int F, float* d_X, void* stream) {
+  MW_CHECK_ARG(d_idx && d_rank2pix && d_slots && d_ovf && d_X && S > 0 && F > 0,
+               "mw_sample_overflow: bad args");
   hipStream_t st = as_stream(stream);
-  const int grid = (int)std::min<int64_t>((S + 255) / 256, 8192);
-  hipLaunchKernelGGL(sample_fixup_kernel, dim3(grid), dim3(256), 0, st, d_pix, d_head, S, F, d_X);
+  const int grid = (int)std::min<int64_t>((S / 64 + 255) / 256 + 1, 1024);
+  hipLaunchKernelGGL(sample_overflow_kernel, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, d_slots, d_ovf,
+                     F, d_X);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
@@ -950,13 +959,13 @@ static int blur_epi_dispatch(const void* d_img, int dtype, int H, int W, int C, 
 }
 
 int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
-                   float pseudoval, const float* h_w, int radius, const int32_t* d_head, int64_t S,
+                   float pseudoval, const float* h_w, int radius, const int32_t* d_slots, int64_t S,
                    const int32_t* d_feat, int F, float* d_X, void* stream) {
-  MW_CHECK_ARG(d_img && d_inv_mean && h_w && d_head && d_feat && d_X, "mw_blur_sample: null pointer");
+  MW_CHECK_ARG(d_img && d_inv_mean && h_w && d_slots && d_feat && d_X, "mw_blur_sample: null pointer");
   MW_CHECK_ARG(H > 0 && W > 0 && C > 0 && F > 0 && S > 0 && S < 0x7fffffffll,
                "mw_blur_sample: bad shape");
   BlurEpi ep{};
-  ep.head = d_head;
+  ep.slots = d_slots;
   ep.S = S;
   ep.X = d_X;
   ep.F = F;

@@ -361,9 +361,11 @@ def blur_gather_fused(img: torch.Tensor, sigma: float, inv_mean, pseudoval: floa
                       feat: torch.Tensor, idx: torch.Tensor, r2p: torch.Tensor, X_out: torch.Tensor,
                       truncate: float = 4.0) -> bool:
     """X_out[j] = blur(lognorm(img))[r2p[idx[j]], feat] without storing the
-    blurred slide: sample map → blur with the sample epilogue → copies for
-    repeated draws.  False (nothing done) when the fused kernel does not take
-    this shape; the caller then materialises the blur and gathers."""
+    blurred slide: sample map (per pixel its first two sample slots, later
+    draws on an overflow list) → blur with the sample epilogue, which writes
+    both table slots → overflow copies.  False (nothing done) when the fused
+    kernel does not take this shape; the caller then materialises the blur
+    and gathers."""
     H, W, C = img.shape
     S, F = X_out.shape
     if S == 0 or inv_mean is None:
@@ -371,18 +373,18 @@ def blur_gather_fused(img: torch.Tensor, sigma: float, inv_mean, pseudoval: floa
     w = gaussian_taps(sigma, truncate)
     r = (len(w) - 1) // 2
     n = H * W
-    head = WS.get("sample_head", 4 * N.query("mw_sample_head_elems", n))
-    pix = WS.get("sample_pix", 4 * S)
+    slots = WS.get("sample_slots", 4 * N.query("mw_sample_slot_elems", n))
+    ovf = WS.get("sample_ovf", 4 * (S + 1))
     st = stream()
     with profiling.timed("sample_map", S * 16):
-        N.call("mw_sample_map", P(idx), P(r2p), S, n, P(head), P(pix), st)
+        N.call("mw_sample_map", P(idx), P(r2p), S, n, P(slots), P(ovf), st)
     with profiling.timed("blur_sample", n * C * img.element_size() + S * F * 4):
         ok = N.try_call("mw_blur_sample", P(img), dtype_code(img), H, W, C, P(inv_mean),
-                        float(pseudoval), w.ctypes.data, r, P(head), S, P(feat), F, P(X_out), st)
+                        float(pseudoval), w.ctypes.data, r, P(slots), S, P(feat), F, P(X_out), st)
     if not ok:
         return False
-    with profiling.timed("sample_fixup", S * 8):
-        N.call("mw_sample_fixup", P(pix), P(head), S, F, P(X_out), st)
+    with profiling.timed("sample_overflow", S * 0):
+        N.call("mw_sample_overflow", P(idx), P(r2p), P(slots), P(ovf), S, F, P(X_out), st)
     FUSED_USED["sample"] += 1
     return True
 

@@ -29,6 +29,12 @@ for mode in ${BENCH_MODES:-}; do
   rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/ab/bench_fused$mode.err; exit $rc; }
   python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('bench ms', round(d['ms_per_step'],3), {k:v['total_ms_per_step'] for k,v in d['kernels'].items()}, d['roofline']['kernel'], round(d['roofline']['frac'],3))" gpurun_out/ab/bench_fused$mode.json
 done
+for da in ${C5_MODES:-}; do
+  echo "[gpu] config-5 slice (40k^2 x 50) MW_DEFERRED_ASSIGN=$da"
+  timeout -k 10 400 env MW_DEFERRED_ASSIGN=$da python bench.py --size 40000 --channels 50 --steps ${C5_STEPS:-2} --warmup 1 --no-cpu-baseline > gpurun_out/ab/bench_c5_$da.json 2> gpurun_out/ab/bench_c5_$da.err
+  rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/ab/bench_c5_$da.err; exit $rc; }
+  python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('c5 ms', round(d['ms_per_step'],1), {k:v['total_ms_per_step'] for k,v in d['kernels'].items()}, d['roofline']['kernel'], round(d['roofline']['frac'],3))" gpurun_out/ab/bench_c5_$da.json
+done
 if [ -n "$PROF" ]; then
   echo "[gpu] rocprof bench MW_FUSED_BLUR=$PROF"
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 env MW_FUSED_BLUR=$PROF rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/ab/prof" -o bench -- python "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/ab/prof_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/ab/prof.err" ) || { tail -5 gpurun_out/ab/prof.err; exit 1; }
