@@ -104,25 +104,31 @@ def cpu_baseline(size, C, k):
                        f"{threads}")
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, suffix=""):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3
-    FETCH_SIZE / WRITE_SIZE summary (profiles/*/pmc_traffic_*.json, written by
-    tools/pmc_traffic.py from tools/gpu/pmc_bench.sh's separate counter passes over
-    this same bench command; corrections in that file)."""
+    FETCH_SIZE / WRITE_SIZE summary for this workload (profiles/*/pmc_traffic
+    {suffix}_v*.json: "" config 2, "_c5" the config-5 slice; written by
+    tools/pmc_traffic.py from tools/gpu/pmc_bench.sh's separate counter passes
+    over this same bench command; corrections in that file), plus the kernel's
+    SQ summary (issue / wait fractions, VALU and MFMA busy) when recorded.
+    Returns (bytes or None, source or None, counters or None)."""
     import glob
     import re
 
     def ver(f):
-        m = re.search(r"r(\d+)/pmc_traffic_v(\d+)\.json$", f)
+        m = re.search(r"r(\d+)/pmc_traffic%s_v(\d+)\.json$" % re.escape(suffix), f)
         return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic_v*.json")), key=ver)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_traffic{suffix}_v*.json")), key=ver)
     if not files:
-        return None, None
-    rec = json.load(open(files[-1])).get("kernels", {}).get(kernel)
+        return None, None, None
+    d = json.load(open(files[-1]))
+    rec = d.get("kernels", {}).get(kernel)
+    sq = d.get("sq", {}).get(kernel)
+    src = os.path.relpath(files[-1], ROOT)
     if not rec or not rec.get("calibrated", False):
-        return None, None
-    return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+        return None, (src if sq else None), sq
+    return rec["traffic_bytes"], src, sq
 
 
 def _free_port() -> int:
@@ -256,7 +262,7 @@ def main():
                         key=lambda kv: kv[1]["total_ms"])
     per_launch_bytes = dom["bytes"] / max(dom["count"], 1)
     achieved = per_launch_bytes / (dom["mean_ms"] * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(dom_name)
+    traffic, traffic_src, counters = pmc_traffic(dom_name, "_c5" if (H, W, C) == (40000, 40000, 50) else "")
     # SURVEY §8(d) whole-pipeline algorithmic bytes (per slide)
     N_pix, F, k = H * W, C, args.k
     B = (N_pix * C * 2 + (N_pix * C * 2 + N_pix + S * F * 4) + (k + n_iter + 1) * S * F * 4
@@ -283,6 +289,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "counters": counters,
                      "launches": dom["count"], "avg_launch_ms": dom["mean_ms"],
                      "algorithmic_bytes_per_launch": per_launch_bytes},
         "pipeline_roofline": {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,

@@ -95,13 +95,20 @@ __global__ void argmax_final_kernel(const double* __restrict__ pv, const int64_t
 __host__ __device__ inline size_t assign_wave_bytes(int k, int CMAX) {
   return (size_t)(k + 1) * 64 * 12 + (size_t)64 * CMAX * 4;
 }
+// XL: the wave's tile (64 x C floats, CMAX floats of readable pad: the last
+// row's pair reads past C), reused for the per-lane sums at the end
+constexpr int kAssignXLK = 8;  // XL keeps the per-label sums in registers: k <= 8
+__host__ __device__ inline size_t assign_wave_bytes_xl(int k, int C, int CMAX) {
+  const size_t tile = (size_t)64 * C * 4 + (size_t)CMAX * 4, sums = (size_t)(k + 1) * 64 * 12;
+  return ((tile > sums ? tile : sums) + 15) & ~(size_t)15;
+}
 // KMeans.predict + estimate_confidence_score_mxif (MILWRM.py:237-277,
 // 389-450) over every pixel of an HWC image: label of the nearest center
 // (strict argmin, same packed-FMA distance as the Lloyd E-step), confidence
 // (d2 - d1) / d2 from the two smallest distances, -1 / NaN outside the mask.
 // Per-block record: [sum conf k | count k] (fp64, fixed combine order).
 // Waves stream 64-pixel tiles (64*C floats) with the next tile in flight.
-template <int CMAX, int KS, bool SC>
+template <int CMAX, int KS, bool SC, bool XL = false>
 __global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float* __restrict__ img, int C,
                                                      const int32_t* __restrict__ feat, int F,
                                                      const float* __restrict__ ga,
@@ -123,11 +130,19 @@ __global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float*
   const size_t cent_bytes = SC ? 0 : cent_t_bytes(KS, CMAX);
   __shared__ int s_ident;
   // per wave: conf sums fp64 [k+1][64] | counts u32 [k+1][64] | tile [64*CMAX]
-  const size_t wslot = assign_wave_bytes(k, CMAX);
+  // (XL: the tile, then the sums written over it from registers at the end)
+  const size_t wslot = XL ? assign_wave_bytes_xl(k, C, CMAX) : assign_wave_bytes(k, CMAX);
   char* wb = smem + cent_bytes + (size_t)wid * wslot;
   double* w_csum = reinterpret_cast<double*>(wb);
   unsigned* w_ccnt = reinterpret_cast<unsigned*>(w_csum + (k + 1) * 64);
-  float* s_tile = reinterpret_cast<float*>(w_ccnt + (k + 1) * 64);
+  float* s_tile = XL ? reinterpret_cast<float*>(wb) : reinterpret_cast<float*>(w_ccnt + (k + 1) * 64);
+  double r_cs[XL ? kAssignXLK + 1 : 1];
+  unsigned r_cc[XL ? kAssignXLK + 1 : 1];
+#pragma unroll
+  for (int j = 0; j < (XL ? kAssignXLK + 1 : 1); ++j) {
+    r_cs[j] = 0.0;
+    r_cc[j] = 0u;
+  }
   if (!SC) load_centers_T<CMAX, KS>(gc, k, F, s_cT);
   if (t == 0) s_ident = F == C;
   __syncthreads();
@@ -137,10 +152,13 @@ __global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float*
     s_b[f] = f < F ? gb[f] : 0.f;
     if (f < F && feat[f] != f) s_ident = 0;  // features = all channels in order
   }
-  for (int q = lane; q < (k + 1) * 64; q += 64) {
-    w_csum[q] = 0.0;
-    w_ccnt[q] = 0u;
-  }
+  if (!XL)
+    for (int q = lane; q < (k + 1) * 64; q += 64) {
+      w_csum[q] = 0.0;
+      w_ccnt[q] = 0u;
+    }
+  else  // the pad past the tile: the last row's pair reads beyond C land here (finite: 0)
+    for (int q = 64 * C + lane; q < 64 * C + CMAX; q += 64) s_tile[q] = 0.f;
   __syncthreads();
 
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(n, lo + R);
@@ -170,11 +188,21 @@ __global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float*
     {
       f4v* s4 = reinterpret_cast<f4v*>(s_tile);
 #pragma unroll
-      for (int i = 0; i < NV; ++i) s4[lane + i * 64] = vv[i];
+      for (int i = 0; i < NV; ++i)  // XL: the slot holds 64 * C floats (+ pad), not 64 * CMAX
+        if (!XL || (lane + i * 64) * 4 < 64 * C) s4[lane + i * 64] = vv[i];
     }
     wt_tail(np * C, p0 * C, n4, img, total, s_tile, lane);
     const int mk = mm;
-    fetch(vv, mm, tc + 2 * nw);
+    fetch(vv, mm, tc + (XL ? 1 : 2) * nw);  // XL: one tile in flight per wave (more waves)
+    float m1, m2;
+    int lab;
+    if constexpr (XL) {  // the scaled row stays in LDS (SC centers): CMAX VGPRs fewer
+      int z = 0;
+      asm volatile("" : "+s"(z));
+      nearest_centers_ls<CMAX, KS, true>(s_tile + lane * C, C, ident, s_feat + z,
+                                          reinterpret_cast<const f2v*>(s_a) + z,
+                                          reinterpret_cast<const f2v*>(s_b) + z, gT, k, lab, m1, m2);
+    } else {
     f2v x2[CMAX / 2];
     if (ident) {
       load_scaled_row<CMAX>(s_tile, lane, C, s_a, s_b, x2);
@@ -189,12 +217,11 @@ __global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float*
       for (int p = 0; p < CMAX / 2; ++p)
         x2[p] = __builtin_elementwise_fma(f2v{xs[sf[2 * p]], xs[sf[2 * p + 1]]}, sa[p], sb[p]);
     }
-    float m1, m2;
-    int lab;
     if (SC)
       nearest_centers_s<CMAX, KS, true>(x2, gT, k, lab, m1, m2);
     else
       nearest_centers<CMAX, KS, true>(x2, s_cT, k, lab, m1, m2);
+    }
     const bool valid = lane < np;
     const bool in_mask = valid && mk != 0;
     const float conf = in_mask ? (m2 - m1) / m2 : __builtin_nanf("");
@@ -205,22 +232,45 @@ __global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float*
     }
     // per-label sum of confidences and counts: lane-private LDS slots in a
     // fixed order (pixels outside the mask/tile go to the sink slot k)
-    {
+    if constexpr (XL) {  // the same per-slot add sequence, in registers (x + 0.0 == x)
+      const int sl = lab < 0 ? k : lab;
+      const double cv = in_mask ? (double)conf : 0.0;
+#pragma unroll
+      for (int j = 0; j <= kAssignXLK; ++j) {
+        r_cs[j] += sl == j ? cv : 0.0;
+        r_cc[j] += sl == j ? 1u : 0u;
+      }
+    } else {
       const int slot = (lab < 0 ? k : lab) * 64 + lane;
       atomicAdd(&w_csum[slot], in_mask ? (double)conf : 0.0);
       atomicAdd(&w_ccnt[slot], 1u);
     }
   };
-  f4v va[NV], vb[NV];
-  int ma = 0, mb = 0;
   int tc = wid;
-  if (tc < ntile) {
-    fetch(va, ma, tc);
-    fetch(vb, mb, tc + nw);
+  if constexpr (XL) {
+    f4v va[NV];
+    int ma = 0;
+    if (tc < ntile) fetch(va, ma, tc);
+    for (; tc < ntile; tc += nw) body(va, ma, tc);
+  } else {
+    f4v va[NV], vb[NV];
+    int ma = 0, mb = 0;
+    if (tc < ntile) {
+      fetch(va, ma, tc);
+      fetch(vb, mb, tc + nw);
+    }
+    for (; tc < ntile; tc += 2 * nw) {
+      body(va, ma, tc);
+      if (tc + nw < ntile) body(vb, mb, tc + nw);
+    }
   }
-  for (; tc < ntile; tc += 2 * nw) {
-    body(va, ma, tc);
-    if (tc + nw < ntile) body(vb, mb, tc + nw);
+  if constexpr (XL) {  // lane-private slots, as the LDS-sum form leaves them
+#pragma unroll
+    for (int j = 0; j <= kAssignXLK; ++j)
+      if (j <= k) {
+        w_csum[j * 64 + lane] = r_cs[j];
+        w_ccnt[j * 64 + lane] = r_cc[j];
+      }
   }
   __syncthreads();
   double* out = rec + (size_t)blockIdx.x * 2 * k;
@@ -363,17 +413,27 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
     return e ? atoi(e) : 8;
   }();
   const bool sc = k <= sc_k;
+  static const bool xl = [] {  // scaled row re-read from LDS (MW_ASSIGN_XL=0: held in registers)
+    const char* e = getenv("MW_ASSIGN_XL");
+    return !(e && e[0] == '0');
+  }();
 #define MW_AS2(CM, KSV, SCV)                                                                    \
   {                                                                                             \
     const size_t cent = SCV ? 0 : cent_t_bytes(KSV, CM);                                        \
-    const int nw = assign_waves(k, C);                                                          \
-    const size_t lds = cent + nw * assign_wave_bytes(k, CM);                                    \
+    const bool xlv = SCV && CM >= 32 && xl && k <= kAssignXLK;                                  \
+    const int nw = xlv ? 4 : assign_waves(k, C);                                                \
+    const size_t lds = cent + nw * (xlv ? assign_wave_bytes_xl(k, C, CM) : assign_wave_bytes(k, CM)); \
     if (lds > 160 * 1024) {                                                                     \
       set_error("mw_assign_conf: LDS %zu too large (C=%d k=%d)", lds, C, k);                    \
       return MW_EUNSUPPORTED;                                                                   \
     }                                                                                           \
-    hipLaunchKernelGGL((assign_kernel<CM, KSV, SCV>), dim3(G), dim3(64 * nw), lds, s, d_img, C, \
-                       d_feat, F, d_a, d_b, d_centers, gT, k, d_mask, n_pix, R, d_label, d_conf, rec); \
+    if (xlv)                                                                                    \
+      hipLaunchKernelGGL((assign_kernel<CM, KSV, SCV, SCV && (CM >= 32)>), dim3(G), dim3(64 * nw), lds, s, \
+                         d_img, C, d_feat, F, d_a, d_b, d_centers, gT, k, d_mask, n_pix, R, d_label, \
+                         d_conf, rec);                                                          \
+    else                                                                                        \
+      hipLaunchKernelGGL((assign_kernel<CM, KSV, SCV>), dim3(G), dim3(64 * nw), lds, s, d_img, C, \
+                         d_feat, F, d_a, d_b, d_centers, gT, k, d_mask, n_pix, R, d_label, d_conf, rec); \
   }
 #define MW_AS(CM, KSV)                                                                          \
   {                                                                                             \

@@ -240,6 +240,63 @@ __device__ __forceinline__ void nearest_centers_s(const f2v (&x2)[FMAX / 2],
   }
 }
 
+// nearest_centers_s without the scaled row in registers: each pass over a
+// group of four centers re-reads the row from the wave's LDS tile and scales
+// it (the same fma as load_scaled_row, so the same x and bitwise the same
+// distances), which frees FMAX VGPRs for more waves per SIMD (the label pass
+// at C = 50 held 270 VGPRs: one wave per SIMD, latency-bound).  `xs` = this
+// lane's row in LDS (F floats), `sf` the feature channels (identity: pairs
+// read as 8-byte words when F is even).
+template <int FMAX, int KS, bool TOP2>
+__device__ __forceinline__ void nearest_centers_ls(const float* xs, int F, bool ident, const int* sf,
+                                                   const f2v* sa, const f2v* sb,
+                                                   const f2v* __restrict__ gT, int k, int& lab,
+                                                   float& m1, float& m2) {
+  constexpr int NP = FMAX / 2;
+  const bool pairs = ident && (F & 1) == 0;
+  const f2v* xp = reinterpret_cast<const f2v*>(xs);  // 8-byte aligned when pairs (F even)
+  lab = 0;
+  m1 = 0.f;
+  m2 = __builtin_inff();
+  for (int j0 = 0; j0 < k; j0 += 4) {
+    f2v acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f2v{0.f, 0.f};
+    if (pairs) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const f2v x = __builtin_elementwise_fma(xp[p], sa[p], sb[p]);
+        const f2v* cp = gT + p * KS + j0;
+        const f2v c[4] = {cp[0], cp[1], cp[2], cp[3]};
+        dist4_s(x, c, acc);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const f2v x = __builtin_elementwise_fma(f2v{xs[sf[2 * p]], xs[sf[2 * p + 1]]}, sa[p], sb[p]);
+        const f2v* cp = gT + p * KS + j0;
+        const f2v c[4] = {cp[0], cp[1], cp[2], cp[3]};
+        dist4_s(x, c, acc);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = j0 + q;
+      if (j < k) {
+        const float dd = acc[q].x + acc[q].y;
+        if (TOP2) {
+          if (j == 0) { m1 = dd; lab = 0; }
+          else if (dd < m1) { m2 = m1; m1 = dd; lab = j; }
+          else if (dd < m2) { m2 = dd; }
+        } else if (j == 0 || dd < m1) {
+          m1 = dd;
+          lab = j;
+        }
+      }
+    }
+  }
+}
+
 // pair-major image (FMAX/2 x KS float pairs) of k x F row-major centers in
 // global memory, for nearest_centers_s
 template <int FMAX, int KS>

@@ -18,7 +18,9 @@ import sys
 
 # bench.py profiling names -> substring of the HIP kernel symbol
 KERNELS = {
-    "blur": "blur_mfma_kernel<",
+    "blur": "true, 0>(",           # blur_mfma_kernel<T, R, CT, BT, true, kEpiStore>
+    "blur_sample": "true, 1>(",    # ... kEpiSample (deferred blur: rows written by the blur)
+    "blur_assign": "true, 2>(",    # ... kEpiAssign (deferred blur: labels written by the blur)
     "assign_conf": "assign_kernel<",
     "kpp_init": "kpp_pass_kernel<32, 1, 0>",
     "kpp_step1": "kpp_pass_kernel<32, 4, 1>",
@@ -27,11 +29,20 @@ KERNELS = {
     "lloyd_pass_mode0_tile": "lloyd_pass_kernel<32, 0, 1, 1>",
     "lloyd_pass_mode1": "lloyd_pass_kernel<32, 1, 0, 1>",
     "lloyd_pass_mode2": "lloyd_pass_kernel<32, 2, 0, 1>",
-    "gather": "gather_kernel<",
-    "nz_stats": "nz_stats_kernel<",
+    "kpp_init_f64": "kpp_pass_kernel<64, 1, 0>",
+    "kpp_step1_f64": "kpp_pass_kernel<64, 4, 1>",
+    "kpp_step_f64": "kpp_pass_kernel<64, 4, 2>",
+    "lloyd_first_f64": "lloyd_pass_kernel<64, 0, 0, 1>",
+    "lloyd_tile_f64": "lloyd_pass_kernel<64, 0, 1, 1>",
+    "lloyd_queue_f64": "lloyd_pass_kernel<64, 0, 2, 1>",
+    "lloyd_final_f64": "lloyd_pass_kernel<64, 1, 0, 1>",
+    "sample_map": "sample_map_kernel",
+    "col_stats": "gather_kernel<false>",
+    "gather": "gather_kernel<true>",
+    "nz_stats": "nz_stats_u16_kernel",
     "mask_scatter": "mask_scatter_kernel",
 }
-UNCALIBRATED = {"gather"}  # 120-B random rows, not a wide coalesced stream
+UNCALIBRATED = {"gather", "blur_sample", "sample_map"}  # random rows / atomics: not wide coalesced streams
 
 
 def per_launch(path, pat):
