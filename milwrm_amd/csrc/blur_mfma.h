@@ -722,18 +722,22 @@ static int launch_blur_mfma_rc(const T* in, int H, int W, int C, const float* in
 template <typename T, int R>
 static int launch_blur_mfma_r(const T* in, int H, int W, int C, const float* inv_mean, float p,
                               const BlurTaps& taps, float* out, hipStream_t st) {
-  // column tiles per band: 8 (128-column bands, one 16-wave workgroup per CU)
-  // for C <= 32, where the 16 halo columns cost 12.5 % of the input instead of
-  // 25 % (3.91-3.93 vs 4.04-4.06 ms at 10k^2 x 30, same box, bitwise the same
-  // output); 4 for wider slides.  MW_BLUR_BT=4 forces 64-column bands.
+  // column tiles per band: 4 (64-column bands, two 8-wave workgroups per CU
+  // at C <= 32).  128-column bands (one 16-wave workgroup per CU, 12.5 % halo
+  // instead of 25 %) are 3 % faster in a blur-only loop (3.91-3.93 vs
+  // 4.04-4.06 ms) but 1.5-2.5 % slower inside the bench step (4.02-4.07 vs
+  // 3.96-3.98 ms, same box, tools/dev/r3_bt_sweep.sh); development builds
+  // (-DMW_BLUR_BT8) keep them behind MW_BLUR_BT=8.
+  const BlurEpi ep{};
+#ifdef MW_BLUR_BT8
   static const int bt = [] {
     const char* e = getenv("MW_BLUR_BT");
-    return (e && atoi(e) == 4) ? 4 : 8;
+    return (e && atoi(e) == 8) ? 8 : 4;
   }();
-  const BlurEpi ep{};
   if (bt == 8 && C <= 32)
     return C <= 16 ? launch_blur_mfma_rc<T, R, 1, 8, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st)
                    : launch_blur_mfma_rc<T, R, 2, 8, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
+#endif
   if (C <= 16) return launch_blur_mfma_rc<T, R, 1, 4, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
   if (C <= 32) return launch_blur_mfma_rc<T, R, 2, 4, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
   if (C <= 48) return launch_blur_mfma_rc<T, R, 3, 4, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);

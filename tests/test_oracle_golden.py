@@ -65,6 +65,56 @@ def test_kmeans_plusplus_indices(golden):
         np.testing.assert_array_equal(idx, g["kpp_indices"][k, :k])
 
 
+def _kpp_margins(X, k, seed=18):
+    """Per k-means++ step (sklearn _kmeans.py:225-272 on centered X): the
+    relative distance of every target u * pot to the cumulative-sum
+    boundaries around the row it selects, and the relative gap between the
+    best and second-best trial potentials (distinct candidates)."""
+    n = X.shape[0]
+    rs = np.random.RandomState(seed)
+    T = 2 + int(np.log(k))
+    x_sq = np.einsum("ij,ij->i", X, X)
+    closest = O._sq_dist_gemm(X, X[[rs.choice(n, p=np.ones(n) / n)]], x_sq)[:, 0]
+    pot = closest.sum()
+    out = []
+    for _ in range(1, k):
+        rv = rs.uniform(size=T) * pot
+        cum = np.cumsum(closest)
+        cand = np.minimum(np.searchsorted(cum, rv), n - 1)
+        lo = np.where(cand > 0, cum[cand - 1], 0.0)
+        cmarg = float((np.minimum(np.abs(cum[cand] - rv), np.abs(rv - lo)) / pot).min())
+        d = O._sq_dist_gemm(X, X[cand], x_sq).T
+        np.minimum(closest, d, out=d)
+        pots = d.sum(axis=1)
+        o = np.argsort(pots, kind="stable")
+        gap = float((pots[o[1]] - pots[o[0]]) / pots[o[0]]) if cand[o[1]] != cand[o[0]] else np.inf
+        out.append((cmarg, gap))
+        b = int(np.argmin(pots))
+        pot, closest = pots[b], d[b]
+    return out
+
+
+def test_kpp_decision_margins(golden):
+    """Round-2 DESIGN recorded a reverted k-means++ variant whose golden
+    indices changed at k = 12 (cause not found) and the verdict asked whether
+    index parity hangs on fp64 summation order.  It does not on this fixture:
+    every decision of every k = 2..20 seeding sits >= 1.7e-6 relative from its
+    boundary (target vs cumulative sum) and >= 4.7e-4 between the best two
+    trial potentials -- ten orders of magnitude above any reordering of fp64
+    sums (~1e-15), so a flip there means different distances (a defect of
+    that variant), not rounding.  What the margins are comparable to is the
+    fp32 storage of the clustering rows (~6e-8 per element, the design's
+    documented precision): at n rows a target's margin scales like 1/n."""
+    g = golden("mxif_small")
+    X = g["cluster_data"]
+    Xc = X - X.mean(axis=0)
+    cm, sg = np.inf, np.inf
+    for k in range(2, 21):
+        for c, s in _kpp_margins(Xc, k):
+            cm, sg = min(cm, c), min(sg, s)
+    assert cm > 1e-6 and sg > 4e-4, (cm, sg)
+
+
 def test_first_center_closed_form_vs_numpy():
     for n in (1, 7, 6297, 100003, 2**20):
         rs = np.random.RandomState(18)
