@@ -25,6 +25,8 @@ the host-side logic (tests/test_dist_gloo.py).
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -214,9 +216,11 @@ class DistComm(LocalComm):
         chosen_rows = [msg[0, 1:]]
         eng.init(msg[0, 1:].float().contiguous())
         cand = None
+        self.kpp_host_ms = []  # per step: host time from the sync to the next trial pass queued
         for c in range(1, k + 1):
             n_arr = 1 if c == 1 else T
             g = self.all_gather_t(eng.pots_t(c, n_arr))  # [world, n_arr]: the step's one sync
+            t_sync = time.perf_counter()
             tot = np.zeros(n_arr)
             for r in range(self.world):
                 tot = tot + g[r]
@@ -230,6 +234,7 @@ class DistComm(LocalComm):
                                    g[:, best], self.rank)
             cand = self._owned_rows(eng, eng.search_t(c, best, rv_local), off)
             eng.trial(c, best, cand[:, 1:].float().contiguous())
+            self.kpp_host_ms.append((time.perf_counter() - t_sync) * 1e3)
         out = torch.cat([torch.stack(chosen)[:, None], torch.stack(chosen_rows)], 1).cpu().numpy()
         return (out[:, 1:] - rows.mu) * rows.inv, out[:, 0].astype(np.int64)
 

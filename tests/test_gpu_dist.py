@@ -49,6 +49,7 @@ def _run(slides, batches, comm):
                inertia=lab.kmeans.inertia_, rows_labels=lab.kmeans.labels_,
                tid=[np.nan_to_num(t, nan=-1) for t in lab.tissue_IDs],
                cid=[np.nan_to_num(c, nan=-1) for c in lab.confidence_IDs])
+    out["kpp_host_ms"] = list(getattr(comm, "kpp_host_ms", []))
     lab.find_optimal_k(random_state=18, alpha=0.05)
     out["best_k"] = int(lab.k)
     out["curve"] = lab.inertia_curve_["Scaled Inertia"].values
@@ -98,6 +99,11 @@ def test_two_shards_bitwise_equal_single_process(gpu):
         for key in ("mean", "scale", "idx", "centers", "curve"):
             np.testing.assert_array_equal(g[key], ref[key], err_msg=key)
         assert g["n_iter"] == ref["n_iter"]
+        # host time per sharded k-means++ step (sync -> next trial pass queued:
+        # targets, owner search, the candidate all-reduce over gloo)
+        ms = g["kpp_host_ms"]
+        assert len(ms) == 5 and max(ms) < 50.0, ms
+        print(f"rank {r}: sharded k-means++ host time per step {np.mean(ms):.2f} ms (max {max(ms):.2f})")
         assert g["inertia"] == ref["inertia"]
         assert g["best_k"] == ref["best_k"]
         for j, i in enumerate(SHARDS[r]):
