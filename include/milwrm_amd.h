@@ -238,7 +238,10 @@ int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu,
  * `kind` (mode 0): 0 = first pass (every label 255: sums of all rows on the
  * fp64 matrix cores), 1 = stream every row, the bounds skip the E-step per
  * row (most rows undecided), 2 = stream the row state only and read just the
- * undecided rows (few undecided).  Same results for any kind.
+ * undecided rows (few undecided), chunk by chunk in one kernel, 4 = the same
+ * as two kernels: the bound test over the whole row state lists the undecided
+ * rows, then a second launch reads only those (falls back to 2 when S >= 2^31;
+ * ws then also holds the lists).  Same results for any kind.
  * k <= 64, F <= 64, n <= 24.  h_fits is a host array. */
 typedef struct mw_lloyd_fit {
   const float* centers;

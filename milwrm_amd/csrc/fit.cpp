@@ -520,12 +520,16 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
       const char* e = getenv("MW_LLOYD_QUEUE_BELOW");
       return e ? atof(e) : 0.3;  // as kmeans.QUEUE_BELOW
     }();
+    static const int queue_kind = [] {  // MW_LLOYD_LIST=0: one-kernel kQueue (A/B)
+      const char* e = getenv("MW_LLOYD_LIST");
+      return (e && e[0] == '0') ? 2 : 4;  // as kmeans.QUEUE_KIND
+    }();
     int kind = first_kind;  // first pass
     if (last_recomputed >= 0) {
       double frac = (double)last_recomputed / (double)S;
       if (fit.prev_dmax > 0.f && std::isfinite(fit.drift_max))
         frac *= std::min(1.0, (double)fit.drift_max / (double)fit.prev_dmax);
-      kind = frac > queue_below ? 1 : 2;
+      kind = frac > queue_below ? 1 : queue_kind;
     }
     MW_TRY(fit.pass(0, kind, 0, rec));
     for (size_t i = 0; i < (size_t)k * F; ++i) {

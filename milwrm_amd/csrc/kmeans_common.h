@@ -42,7 +42,9 @@ __host__ __device__ constexpr int kpad4(int k) { return (k + 3) & ~3; }
 // of them to the wave's LDS tile of 64*FMAX floats: floats past 64*F are the
 // following rows' data, read by the E-step only for padded features whose scale
 // is exactly 0.  Floats past the array's last whole float4 are patched with
-// scalar loads in the final tile only.
+// scalar loads in the final tile only.  (The k-means++ and Lloyd passes at
+// FMAX = 64 load and keep only the 64*F floats plus a zeroed pad instead:
+// LDS, not registers, bounds their occupancy there.)
 __device__ __forceinline__ void wt_tail(int nfl, int64_t e0, int64_t n4, const float* __restrict__ X,
                                         int64_t total, float* s, int lane) {
   if (e0 + nfl > n4 * 4) {  // wave-uniform

@@ -154,7 +154,15 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
   double* s_red = reinterpret_cast<double*>(smem);  // [4] block-sum scratch
   const int t = threadIdx.x, lane = t & 63, nw = blockDim.x >> 6;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  float* s_tile = reinterpret_cast<float*>(smem + 64) + (size_t)wid * 64 * FMAX;
+  // per-wave tile of 64 rows x FMAX floats; FMAX = 64 (FS): 64 rows x F
+  // floats (+4: the pair read past an odd-F tile's last row, kept finite) and
+  // the feature loop stops at F, so at F = 50 three blocks fit a CU instead
+  // of two (at F <= 32 the fixed-trip loop is faster: config 2 +0.4 ms)
+  constexpr bool FS = FMAX == 64;
+  const int tstride = FS ? 64 * F + 4 : 64 * FMAX;
+  const int fend = FS ? F : FMAX;
+  float* s_tile = reinterpret_cast<float*>(smem + 64) + (size_t)wid * tstride;
+  if (FS && lane < 4) s_tile[64 * F + lane] = 0.f;
 
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
   const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
@@ -181,7 +189,10 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
     tt = tt < ntile ? tt : ntile - 1;
     if (MODE != 0)
       cur_next = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, lane * 8, tt * 512, 0));
-    tile_load<NV>(rx, tt * tile_bytes, lane, v);
+#pragma unroll
+    for (int i = 0; i < NV; ++i)  // only the vectors that hold the tile's 64 x F floats
+      if (!FS || i * 1024 < tile_bytes)
+        v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16 + i * 1024, tt * tile_bytes, 0));
   };
   int tc = wid;
   if (tc < ntile) fetch(tc);
@@ -191,7 +202,8 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
     {
       f4v* s4 = reinterpret_cast<f4v*>(s_tile);
 #pragma unroll
-      for (int i = 0; i < NV; ++i) s4[lane + i * 64] = v[i];
+      for (int i = 0; i < NV; ++i)
+        if (!FS || (lane + i * 64) * 16 < tile_bytes) s4[lane + i * 64] = v[i];
     }
     wt_tail(nrow * F, r0 * F, n4, X, total, s_tile, lane);
     double cd = cur_next;
@@ -236,7 +248,7 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
         for (int c = 0; c < T; ++c) dot[c] = fma(xs, q.c[c], dot[c]);
       };
       TabF t0 = ld(0), t1 = ld(1);
-      for (int f = 0; f < FMAX; f += 2) {
+      for (int f = 0; f < fend; f += 2) {  // features past F add exact zeros
         const TabF n0 = ld(f + 2), n1 = ld(f + 3);
         const f2v x2 = *reinterpret_cast<const f2v*>(xr + f);
         featt((double)x2.x, t0);
@@ -246,7 +258,7 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
       }
     } else {
 #pragma unroll 4
-      for (int f = 0; f < FMAX; ++f) feat((double)xr[f], f);
+      for (int f = 0; f < fend; ++f) feat((double)xr[f], f);
     }
 #pragma unroll
     for (int c = 0; c < T; ++c) {
@@ -433,7 +445,7 @@ static int kpp_pass_launch(const float* X, int64_t S, int F, const double* mu, c
                      chosen_reset);
   MW_LAUNCH_CHECK();
   const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
-  const size_t lds = 64 + (size_t)4 * 64 * FM * sizeof(float);
+  const size_t lds = 64 + (size_t)4 * (FM == 64 ? 64 * F + 4 : 64 * FM) * sizeof(float);  // the pass's tiles
   const int mode = c == 0 ? 0 : c == 1 ? 1 : 2;
   const double* tab_prev = c >= 1 ? p.tab_of(c - 1) : nullptr;
   double* bs = p.bsum_of(c, T);

@@ -42,6 +42,12 @@ struct LloydFitsArg {
 };
 
 __host__ __device__ inline int lloyd_rec(int k, int F) { return 2 * k * F + k + 4; }
+__host__ __device__ inline size_t lloyd_al256(size_t x) { return (x + 255) & ~(size_t)255; }
+// kList workspace after the G block records: per-block list lengths [G]
+// int32, then per-block lists of undecided row indices [G][R] int32
+__host__ __device__ inline size_t lloyd_list_off(int G, int k, int F) {
+  return lloyd_al256((size_t)G * lloyd_rec(k, F) * sizeof(double));
+}
 
 // x as an exact fixed-point integer: rint(x * 2^e) (|x * 2^e| < 2^41; fp64
 // holds it exactly, and sums of up to 2^12 of them)
@@ -68,8 +74,14 @@ __device__ __forceinline__ float dist_one(const f2v (&x2)[FMAX / 2], const f2v* 
   return acc.x + acc.y;
 }
 
-// bytes of one wave's row tile (64 rows x FMAX floats)
-__host__ __device__ inline size_t lloyd_tile_bytes(int FMAX) { return (size_t)64 * FMAX * 4; }
+// bytes of one wave's row tile: 64 rows x FMAX floats; FMAX = 64: 64 rows x
+// F floats and FMAX - F floats more (zeroed: the padded pairs load_scaled_row
+// reads past the last row), so at F = 50 two blocks fit a CU instead of one
+// (at F <= 32 the full tile loads measured faster)
+__host__ __device__ inline size_t lloyd_tile_bytes(int FMAX, int F) {
+  if (FMAX != 64) return (size_t)64 * FMAX * 4;
+  return (((size_t)64 * F + (FMAX - F) + 3) & ~(size_t)3) * 4;
+}
 
 #ifndef MW_LLOYD_CHUNK
 #define MW_LLOYD_CHUNK 2048  // 4096: 2 blocks per CU (LDS), the sweep's queue passes 15 % slower
@@ -93,7 +105,7 @@ struct alignas(16) LloydSmall {
 __host__ __device__ inline size_t lloyd_lds_bytes(int FMAX, int k, int F, int mode, int kind) {
   size_t b = sizeof(LloydSmall) + cent_t_bytes(64, FMAX);
   if (mode == 0) b += ((size_t)k * F * 8 + 15) & ~(size_t)15;
-  b += 4 * (lloyd_tile_bytes(FMAX) + 64 * 4);
+  b += 4 * (lloyd_tile_bytes(FMAX, F) + 64 * 4);
   if (mode == 0 && kind == 2) b += (size_t)kChunk * 2;  // kQueue
   return b;
 }
@@ -103,6 +115,7 @@ constexpr int kFirst = 0;  // every row unlabelled: full E-step, sums of all row
 constexpr int kTile = 1;   // stream every tile's rows; bounds skip the E-step per lane
 constexpr int kQueue = 2;  // stream only the row state; read the undecided rows
 constexpr int kFirstAtomic = 3;  // kFirst with the sums by LDS atomics (A/B)
+constexpr int kList = 4;  // kQueue as two launches: lloyd_mark_kernel lists, this kernel reads
 
 // One pass of fit g = blockIdx.x % n over row block blockIdx.x / n (the n
 // blocks that read one row block are dispatched together: rows that several
@@ -119,6 +132,10 @@ constexpr int kFirstAtomic = 3;  // kFirst with the sums by LDS atomics (A/B)
 //     row state (4 rows per lane) and queues the rows it cannot decide; waves
 //     gather the queued rows 64 at a time and finish them as kTile does.  For
 //     passes where few rows are undecided.
+//   MODE 0, kList: lloyd_mark_kernel (launched first) ran the bound test over
+//     the block's whole range and listed its undecided rows; waves take the
+//     list 64 rows at a time (state loads issued with the list entries, then
+//     the gather) and finish them as kQueue does, with no block barrier.
 //   MODE 1: full E-step (labels updated) + inertia of the new labels
 //   MODE 2: inertia of the current labels
 template <int FMAX, int MODE, int KIND, int MBT>
@@ -156,11 +173,17 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
   sp += cent_t_bytes(64, FMAX);
   unsigned long long* s_acc = reinterpret_cast<unsigned long long*>(sp);
   if (MODE == 0) sp += ((size_t)k * F * 8 + 15) & ~(size_t)15;
-  float* s_tile = reinterpret_cast<float*>(sp + (size_t)wid * lloyd_tile_bytes(FMAX));
-  sp += 4 * lloyd_tile_bytes(FMAX);
+  const int tile_fl = (int)(lloyd_tile_bytes(FMAX, F) / 4);
+  float* s_tile = reinterpret_cast<float*>(sp + (size_t)wid * tile_fl * 4);
+  sp += 4 * (size_t)tile_fl * 4;
   int* s_lab = reinterpret_cast<int*>(sp) + wid * 64;
   sp += 4 * 64 * 4;
   uint16_t* s_q = reinterpret_cast<uint16_t*>(sp);
+  // tiles and gathers write only the 64 x F floats of a tile; the scaled-row
+  // read of the last row runs past them (padded features, times a zero
+  // scaler), so the rest of the wave's tile buffer must hold finite values,
+  // never stale LDS bits (NaN * 0 = NaN: nondeterministic labels)
+  for (int q = 64 * F + lane; q < tile_fl; q += 64) s_tile[q] = 0.f;
 
   load_centers_T<FMAX, 64>(fit.centers, k, F, s_cT);
   for (int f = t; f < 64; f += blockDim.x) {
@@ -168,7 +191,7 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
     s_b[f] = f < F ? gb[f] : 0.f;
     s_e[f] = f < F ? qexp[f] : 0;
   }
-  constexpr bool BOUNDS = MODE == 0 && (KIND == kTile || KIND == kQueue);
+  constexpr bool BOUNDS = MODE == 0 && (KIND == kTile || KIND == kQueue || KIND == kList);
   for (int j = t; j < 64; j += blockDim.x) {
     s_drift[j] = (BOUNDS && j < k) ? fit.drift[j] : 0.f;
     s_half[j] = (BOUNDS && j < k) ? fit.half_sep[j] : 0.f;
@@ -248,11 +271,6 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
 
   if constexpr (MODE == 0 && KIND == kQueue) {
     // =========================== queue pass ===========================
-    // the gather writes only the 64 x F floats of a batch; the scaled-row
-    // read of the last row runs past them (padded features, times a zero
-    // scaler), so the rest of the wave's tile buffer must hold finite values,
-    // never stale LDS bits (NaN * 0 = NaN: nondeterministic labels)
-    for (int q = 64 * F + lane; q < 64 * FMAX; q += 64) s_tile[q] = 0.f;
     for (int64_t c0 = lo; c0 < hi; c0 += kChunk) {
       const int clen = (int)min((int64_t)kChunk, hi - c0);
       // ---- phase 1: bound test, 4 consecutive rows per lane, queue the undecided ----
@@ -377,6 +395,67 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
       if (t == 0) s_qn = 0;
       __syncthreads();
     }
+  } else if constexpr (MODE == 0 && KIND == kList) {
+    // ============================ list pass =============================
+    const int G = (int)(gridDim.x / n);
+    const char* wsb = reinterpret_cast<const char*>(fit.ws);
+    const size_t loff = lloyd_list_off(G, k, F);
+    const int nq = reinterpret_cast<const int*>(wsb + loff)[blk];
+    const int* __restrict__ list =
+        reinterpret_cast<const int*>(wsb + loff + lloyd_al256((size_t)G * 4)) + (size_t)blk * R;
+    int* s_row = s_lab;  // the batch's 64 row indices (per wave)
+    for (int e0 = wid * 64; e0 < nq; e0 += nw * 64) {
+      const int cnt_b = min(64, nq - e0);
+      const bool valid = lane < cnt_b;
+      const int64_t r = list[e0 + (valid ? lane : 0)];
+      // the row state does not depend on the gather: its loads go out first
+      const int lab_old = labels[r];
+      const float ub_in = ubuf[r], lb_in = lbuf[r];
+      s_row[lane] = (int)r;
+      __builtin_amdgcn_wave_barrier();
+      if ((F & 1) == 0) {
+        const int P2 = F >> 1;
+        int j = lane / P2, c = lane - (lane / P2) * P2;  // piece (j, c) = p, stepped by 64
+        const int dj = 64 / P2, dc = 64 - dj * P2;
+        constexpr int kGB = 8;
+        for (int i0 = 0; i0 < P2; i0 += kGB) {
+          f2v v[kGB];
+          int dst[kGB];
+#pragma unroll
+          for (int i = 0; i < kGB; ++i) {
+            const bool ok = i0 + i < P2;
+            const int64_t rj = s_row[j < cnt_b ? j : 0];
+            v[i] = ok ? *reinterpret_cast<const f2v*>(X + rj * F + 2 * c) : f2v{0.f, 0.f};
+            dst[i] = ok ? j * F + 2 * c : -1;
+            j += dj;
+            c += dc;
+            if (c >= P2) { c -= P2; ++j; }
+          }
+#pragma unroll
+          for (int i = 0; i < kGB; ++i)
+            if (dst[i] >= 0) *reinterpret_cast<f2v*>(s_tile + dst[i]) = v[i];
+        }
+      } else {
+        for (int p = lane; p < 64 * F; p += 64) {
+          const int j = p / F, c = p - j * F;
+          const int64_t rj = s_row[j < cnt_b ? j : 0];
+          s_tile[j * F + c] = X[rj * F + c];
+        }
+      }
+      const int la = lab_old < k ? lab_old : 0;
+      const float ub = ub_in + s_drift[la];
+      const float lbv = lb_in - dmax;
+      const float thr = fmaxf(lbv, s_half[la]);
+      finish_rows(valid, valid, lab_old, ub, lbv, thr,
+                  [&](bool v, bool ch, int lab, float u, float l) {
+                    if (v) {
+                      if (ch) labels[r] = (uint8_t)lab;
+                      ubuf[r] = u;
+                      lbuf[r] = l;
+                    }
+                  });
+      __builtin_amdgcn_wave_barrier();  // s_row is rewritten by the next batch
+    }
   } else {
     // ========================== streamed tiles ==========================
     const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
@@ -425,7 +504,11 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
         ub_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ru, lane * 4, tt * 256, 0));
         lb_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, lane * 4, tt * 256, 0));
       }
-      tile_load<NV>(rx, tt * tile_bytes, lane, v);
+#pragma unroll
+      for (int i = 0; i < NV; ++i)  // only the vectors that hold the tile's 64 x F floats
+        if (FMAX != 64 || i * 1024 < tile_bytes)
+          v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16 + i * 1024,
+                                                                               tt * tile_bytes, 0));
     };
     int tc = wid;
     if (tc < ntile) fetch(tc);
@@ -438,7 +521,8 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
       {
         f4v* s4 = reinterpret_cast<f4v*>(s_tile);
 #pragma unroll
-        for (int i = 0; i < NV; ++i) s4[lane + i * 64] = v[i];
+        for (int i = 0; i < NV; ++i)
+          if (FMAX != 64 || (lane + i * 64) * 4 < 64 * F) s4[lane + i * 64] = v[i];
       }
       wt_tail(nrow * F, r0 * F, n4, X, total, s_tile, lane);
       fetch(tc + nw);  // the next tile's loads stay in flight during this tile
@@ -546,6 +630,100 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
   }
 }
 
+// kList, first launch: the bound test of every row of the block's range from
+// the row state alone (4 consecutive rows per lane, 4 groups of 256 rows per
+// wave in flight, no barrier until the end).  Decided rows get their drifted
+// bounds written back; undecided rows go to the block's list, in any order
+// (the pass's sums are integer sums and its other outputs are per row).
+__global__ void __launch_bounds__(256) lloyd_mark_kernel(const LloydFitsArg fits, int n, int64_t S,
+                                                         int F, int64_t R) {
+  __shared__ float s_drift[64], s_half[64];
+  __shared__ int s_n;
+  const int g = blockIdx.x % n, blk = blockIdx.x / n, G = (int)(gridDim.x / n);
+  const mw_lloyd_fit& fit = fits.f[g];
+  const int k = fit.k;
+  const int t = threadIdx.x, lane = t & 63, nw = blockDim.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  for (int j = t; j < 64; j += blockDim.x) {
+    s_drift[j] = j < k ? fit.drift[j] : 0.f;
+    s_half[j] = j < k ? fit.half_sep[j] : 0.f;
+  }
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  const float dmax = fit.drift_max;
+  char* wsb = reinterpret_cast<char*>(fit.ws);
+  const size_t loff = lloyd_list_off(G, k, F);
+  int* __restrict__ list = reinterpret_cast<int*>(wsb + loff + lloyd_al256((size_t)G * 4)) + (size_t)blk * R;
+  const uint8_t* __restrict__ labels = fit.labels;
+  float* __restrict__ ubuf = fit.ub;
+  float* __restrict__ lbuf = fit.lb;
+  const int64_t lo = (int64_t)blk * R, hi = min(S, lo + R);
+  constexpr int NI = 4;
+  for (int64_t c0 = lo; c0 < hi; c0 += (int64_t)NI * nw * 256) {
+    uint32_t lab4[NI];
+    f4v ub4[NI], lb4[NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int64_t r0 = c0 + (int64_t)(it * nw + wid) * 256 + 4 * lane;  // a multiple of 4
+      if (r0 + 3 < hi) {
+        lab4[it] = *reinterpret_cast<const uint32_t*>(labels + r0);
+        ub4[it] = *reinterpret_cast<const f4v*>(ubuf + r0);
+        lb4[it] = *reinterpret_cast<const f4v*>(lbuf + r0);
+      } else {
+        lab4[it] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (r0 + i < hi) {
+            lab4[it] = (lab4[it] & ~(0xFFu << (8 * i))) | ((uint32_t)labels[r0 + i] << (8 * i));
+            ub4[it][i] = ubuf[r0 + i];
+            lb4[it][i] = lbuf[r0 + i];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int64_t g0 = c0 + (int64_t)(it * nw + wid) * 256;
+      if (g0 >= hi) break;  // wave-uniform
+      const int64_t r0 = g0 + 4 * lane;
+      bool skip[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int lab_old = (lab4[it] >> (8 * i)) & 0xFF;
+        const int la = lab_old < k ? lab_old : 0;
+        const float ub = ub4[it][i] + s_drift[la];
+        const float lbv = lb4[it][i] - dmax;
+        const float thr = fmaxf(lbv, s_half[la]);
+        const bool valid = r0 + i < hi;
+        const bool need = valid && (lab_old >= k || !(ub * (1.f + kEps) < thr));
+        skip[i] = valid && !need;
+        ub4[it][i] = ub;
+        lb4[it][i] = lbv;
+        const unsigned long long m = __ballot(need);
+        if (m != 0ull) {
+          int qb = 0;
+          if (lane == 0) qb = atomicAdd(&s_n, __popcll(m));
+          qb = __shfl(qb, 0, 64);
+          if (need) list[qb + __popcll(m & ((1ull << lane) - 1ull))] = (int)(r0 + i);
+        }
+      }
+      if (skip[0] && skip[1] && skip[2] && skip[3]) {
+        *reinterpret_cast<f4v*>(ubuf + r0) = ub4[it];
+        *reinterpret_cast<f4v*>(lbuf + r0) = lb4[it];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (skip[i]) {
+            ubuf[r0 + i] = ub4[it][i];
+            lbuf[r0 + i] = lb4[it][i];
+          }
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) reinterpret_cast<int*>(wsb + loff)[blk] = s_n;
+}
+
 // one fit per blockIdx.y: fixed-order fold of its G block records
 __global__ void __launch_bounds__(256) lloyd_reduce_fits_kernel(const LloydFitsArg fits, int G, int F) {
   const mw_lloyd_fit& fit = fits.f[blockIdx.y];
@@ -600,7 +778,8 @@ extern "C" {
 int mw_lloyd_rec_len(int k, int F) { return lloyd_rec(k, F); }
 
 size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
-  return (size_t)kblocks(S) * lloyd_rec(k, F) * sizeof(double) + 256;
+  const int G = kblocks(S);  // records, then the kList lengths and lists
+  return lloyd_list_off(G, k, F) + lloyd_al256((size_t)G * 4) + (size_t)G * krows(S) * 4 + 256;
 }
 
 int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream) {
@@ -635,8 +814,9 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   MW_CHECK_ARG(S > 0 && F > 0 && n >= 1 && n <= kMaxFits, "mw_lloyd_pass: bad shape (1 <= n <= %d)",
                kMaxFits);
   MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_pass: bad mode %d", mode);
-  MW_CHECK_ARG(kind >= 0 && kind <= 3, "mw_lloyd_pass: bad kind %d", kind);
+  MW_CHECK_ARG(kind >= 0 && kind <= 4, "mw_lloyd_pass: bad kind %d", kind);
   if (mode != 0) kind = kFirst;  // modes 1 and 2 stream every tile
+  if (kind == kList && S >= ((int64_t)1 << 31)) kind = kQueue;  // int32 row lists
   LloydFitsArg fits{};
   int kmax = 0;
   for (int g = 0; g < n; ++g) {
@@ -661,6 +841,10 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   // blocks, at most 4 (else the sums go through LDS atomics)
   const int NBF = FM <= 16 ? 1 : FM / 16, MBF = (kmax + 15) / 16;
   if (mode == 0 && kind == kFirst && MBF * NBF > 4) kind = kFirstAtomic;
+  if (mode == 0 && kind == kList) {
+    hipLaunchKernelGGL(lloyd_mark_kernel, grid, dim3(256), 0, s, fits, n, S, F, R);
+    MW_LAUNCH_CHECK();
+  }
 #define MW_LP(FMV, MO, KI, MBV)                                                                        \
   hipLaunchKernelGGL((lloyd_pass_kernel<FMV, MO, KI, MBV>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, \
                      d_qexp, fits, n, R)
@@ -673,6 +857,7 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     }                                                                            \
     else if (kind == kTile) MW_LP(FMV, 0, kTile, 1);                            \
     else if (kind == kFirstAtomic) MW_LP(FMV, 0, kFirstAtomic, 1);              \
+    else if (kind == kList) MW_LP(FMV, 0, kList, 1);                            \
     else MW_LP(FMV, 0, kQueue, 1);                                              \
   } else if (mode == 1) MW_LP(FMV, 1, kFirst, 1);                               \
   else MW_LP(FMV, 2, kFirst, 1);

@@ -337,7 +337,11 @@ class _FitState:
         return a64[None, :] * sums_x + b64[None, :] * cnt[:, None], cnt, tail[0]
 
 
-KIND_FIRST, KIND_TILE, KIND_QUEUE = 0, 1, 2
+KIND_FIRST, KIND_TILE, KIND_QUEUE, KIND_LIST = 0, 1, 2, 4
+# the few-undecided pass: kList (bound test and list in one launch, the listed
+# rows in a second) unless MW_LLOYD_LIST=0 (kQueue: both phases chunk by chunk
+# in one kernel)
+QUEUE_KIND = KIND_QUEUE if os.environ.get("MW_LLOYD_LIST") == "0" else KIND_LIST
 # a mode-0 pass streams every row (kTile) while the previous pass recomputed
 # more than this fraction of the rows, else only the undecided ones (kQueue):
 # the k = 2..20 sweep at 10k^2 x 30 (tools/sweep_bench.py) took 0.77 / 0.69 s
@@ -361,8 +365,8 @@ def _launch_pass(rows, fits_g, mode, kind, par, poff, outs, st, label="lloyd_pas
         arr[i] = N.LloydFit(base, base + k * F * 4, base + (k * F + k) * 4, D.P(fs.labels),
                             D.P(fs.ub), D.P(fs.lb), D.P(fs.ws), D.P(outs[g]), k,
                             float(fs.drift_max), int(fs.iexp))
-        nbytes += S * 9 + (S * F * 4 if (mode or kind != KIND_QUEUE) else 0)
-    tag = "" if mode else ("_first", "_tile", "_queue", "_first_atomic")[kind]
+        nbytes += S * 9 + (S * F * 4 if (mode or kind not in (KIND_QUEUE, KIND_LIST)) else 0)
+    tag = "" if mode else ("_first", "_tile", "_queue", "_first_atomic", "_list")[kind]
     ev = None
     if TRACE is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -454,7 +458,7 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
         frac = fs.history[-1][1] / max(S_glob, 1)
         if fs.prev_dmax > 0 and np.isfinite(fs.drift_max):
             frac *= min(1.0, fs.drift_max / fs.prev_dmax)
-        return KIND_TILE if frac > QUEUE_BELOW else KIND_QUEUE
+        return KIND_TILE if frac > QUEUE_BELOW else QUEUE_KIND
 
     S_glob = S
     if comm.sharded():

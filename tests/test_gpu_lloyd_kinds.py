@@ -1,5 +1,5 @@
 """Lloyd pass kinds are exact: with every bounded pass forced to kTile, or to
-kQueue, or the default mix, the fits equal the plain Lloyd E-step every pass
+kQueue, or to kList (twice), or the default mix, the fits equal the plain Lloyd E-step every pass
 (MW_LLOYD_NOBOUND) bit for bit — labels, centers, n_iter — for k = 8..20 in
 one batched launch, and repeated runs agree.  Regression: the queue pass
 gathers only the F floats of each row into LDS, and the scaled-row read
@@ -38,9 +38,13 @@ def test_pass_kinds_equal_full_estep(gpu, monkeypatch):
     rows = _rows()
     ks = list(range(8, 21))
     out = {}
-    for name, qb, nobound in [("full", -1.0, True), ("tile", -1.0, False), ("queue", 2.0, False),
-                              ("queue_again", 2.0, False), ("default", KM.QUEUE_BELOW, False)]:
+    for name, qb, qk, nobound in [("full", -1.0, KM.KIND_QUEUE, True), ("tile", -1.0, KM.KIND_QUEUE, False),
+                                  ("queue", 2.0, KM.KIND_QUEUE, False), ("queue_again", 2.0, KM.KIND_QUEUE, False),
+                                  ("list", 2.0, KM.KIND_LIST, False),
+                                  ("list_again", 2.0, KM.KIND_LIST, False),
+                                  ("default", KM.QUEUE_BELOW, KM.QUEUE_KIND, False)]:
         monkeypatch.setattr(KM, "QUEUE_BELOW", qb)
+        monkeypatch.setattr(KM, "QUEUE_KIND", qk)
         if nobound:
             monkeypatch.setenv("MW_LLOYD_NOBOUND", "1")
         else:
@@ -48,7 +52,7 @@ def test_pass_kinds_equal_full_estep(gpu, monkeypatch):
         with contextlib.redirect_stdout(sys.stderr):
             fits = KM.fit_many(rows, ks, random_state=18)
         out[name] = [(np.asarray(m.labels_).copy(), m.cluster_centers_.copy(), m.n_iter_) for m in fits]
-    for name in ("tile", "queue", "queue_again", "default"):
+    for name in ("tile", "queue", "queue_again", "list", "list_again", "default"):
         for i, k in enumerate(ks):
             a, b = out["full"][i], out[name][i]
             assert a[2] == b[2], f"k={k} {name}: n_iter {b[2]} vs {a[2]}"

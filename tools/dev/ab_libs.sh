@@ -25,4 +25,13 @@ for r in $(seq 1 ${C5:-0}); do
     python -c "$summ" gpurun_out/ab/c5_$v.json "c5 $v"
   done
 done
+# k sweep (tools/sweep_bench.py) on the main library under each SWEEP_ENVS entry
+# ("-" = no extra env), alternating, SWEEP rounds
+for r in $(seq 1 ${SWEEP:-0}); do
+  for e in ${SWEEP_ENVS:--}; do
+    E=""; [ "$e" = "-" ] || E="$e"
+    timeout -k 10 300 env $E MW_NOOP=1 python tools/sweep_bench.py --size 10000 --reps 1 > gpurun_out/ab/sweep.json 2> gpurun_out/ab/sweep.err || { tail -3 gpurun_out/ab/sweep.err; exit 1; }
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print('sweep', sys.argv[2], round(d['batched']['s'],4), d['batched'].get('kernels_ms'), 'same', d['identical_curve'])" gpurun_out/ab/sweep.json "$e"
+  done
+done
 echo "[ab] done"
