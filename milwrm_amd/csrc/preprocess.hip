@@ -582,6 +582,92 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   }
 }
 
+// mw_col_stats_rows: gather_kernel's statistics over rows already in X (the
+// fused blur sample epilogue wrote them) with the same block / tile / part
+// partition and the same operation order, so the records are identical, but
+// read straight from global memory instead of through an LDS tile: in one
+// step of a part thread's loop the block's threads read nparts consecutive
+// rows (nparts * F floats, coalesced), and the second pass re-reads them from
+// the caches.  Without the 256 x F tile 4 blocks fit a CU at any F (the tile
+// allowed 2 at F = 50); loads go out 8 per thread at a time.
+__global__ void __launch_bounds__(256) col_stats_rows_kernel(const float* __restrict__ X, int F,
+                                                             int64_t S, int64_t R,
+                                                             double* __restrict__ rec) {
+  __shared__ double s_st[4 * 256];
+  const int t = threadIdx.x;
+  const int nparts = 256 / F;
+  const bool st_on = t < nparts * F;
+  const int sf = st_on ? t % F : 0, spart = st_on ? t / F : 0;
+  double n_acc = 0.0, m_acc = 0.0, q_acc = 0.0;
+  float a_acc = 0.0f;
+  const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
+  constexpr int kB = 8;
+  if (st_on) {
+    for (int64_t r0 = lo; r0 < hi; r0 += kTile) {
+      const int nrow = (int)min((int64_t)kTile, hi - r0);
+      const float* __restrict__ xc = X + r0 * F + sf;
+      const int64_t step = (int64_t)nparts * F;
+      double s = 0.0, cnt = 0.0;
+      int r = spart;
+      for (; r + (kB - 1) * nparts < nrow; r += kB * nparts) {
+        float v[kB];
+#pragma unroll
+        for (int i = 0; i < kB; ++i) v[i] = xc[(int64_t)r * F + i * step];
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+          s += (double)v[i];
+          cnt += 1.0;
+          a_acc = fmaxf(a_acc, fabsf(v[i]));
+        }
+      }
+      for (; r < nrow; r += nparts) {
+        const float v = xc[(int64_t)r * F];
+        s += (double)v;
+        cnt += 1.0;
+        a_acc = fmaxf(a_acc, fabsf(v));
+      }
+      if (cnt > 0.0) {
+        const double m = s / cnt;
+        double q = 0.0;
+        r = spart;
+        for (; r + (kB - 1) * nparts < nrow; r += kB * nparts) {
+          float v[kB];
+#pragma unroll
+          for (int i = 0; i < kB; ++i) v[i] = xc[(int64_t)r * F + i * step];
+#pragma unroll
+          for (int i = 0; i < kB; ++i) {
+            const double d = (double)v[i] - m;
+            q += d * d;
+          }
+        }
+        for (; r < nrow; r += nparts) {
+          const double d = (double)xc[(int64_t)r * F] - m;
+          q += d * d;
+        }
+        chan_merge(n_acc, m_acc, q_acc, cnt, m, q);
+      }
+    }
+    s_st[4 * t + 0] = n_acc;
+    s_st[4 * t + 1] = m_acc;
+    s_st[4 * t + 2] = q_acc;
+    s_st[4 * t + 3] = (double)a_acc;
+  }
+  __syncthreads();
+  double* out = rec + (size_t)blockIdx.x * (1 + 3 * F);
+  if (t < F) {
+    double n = 0.0, m = 0.0, q = 0.0, a = 0.0;
+    for (int part = 0; part < nparts; ++part) {
+      const int u = part * F + t;
+      chan_merge(n, m, q, s_st[4 * u], s_st[4 * u + 1], s_st[4 * u + 2]);
+      a = fmax(a, s_st[4 * u + 3]);
+    }
+    if (t == 0) out[0] = n;
+    out[1 + t] = m;
+    out[1 + F + t] = q;
+    out[1 + 2 * F + t] = a;
+  }
+}
+
 // Merge per-block (n, mean, M2) records: n = sum n_b, mean = sum n_b m_b / n,
 // M2 = sum [M2_b + n_b (m_b - mean)^2]  (fixed order; optional prior record).
 // Fixed-order fold of the G per-block Chan records: 16 parts x 64 features
@@ -858,11 +944,16 @@ int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stre
   MW_CHECK_ARG(d_X && d_ws, "mw_col_stats_rows: null pointer");
   MW_CHECK_ARG(S > 0 && F > 0 && F <= 64, "mw_col_stats_rows: bad shape S=%lld F=%d", (long long)S, F);
   hipStream_t st = as_stream(stream);
+#ifdef MW_COL_STATS_LDS  // A/B: the LDS-tile form (gather_kernel without the gather)
   size_t lds = (size_t)kTile * F * sizeof(float);
   if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
   hipLaunchKernelGGL(gather_kernel<false>, dim3(stream_blocks(S)), dim3(256), lds, st, nullptr, F,
                      nullptr, F, nullptr, nullptr, S, rows_per_block(S), const_cast<float*>(d_X),
                      reinterpret_cast<double*>(d_ws));
+#else
+  hipLaunchKernelGGL(col_stats_rows_kernel, dim3(stream_blocks(S)), dim3(256), 0, st, d_X, F, S,
+                     rows_per_block(S), reinterpret_cast<double*>(d_ws));
+#endif
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
