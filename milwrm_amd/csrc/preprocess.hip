@@ -585,12 +585,12 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
 // mw_col_stats_rows: gather_kernel's statistics over rows already in X (the
 // fused blur sample epilogue wrote them) with the same block / tile / part
 // partition and the same operation order, so the records are identical, but
-// read straight from global memory instead of through an LDS tile: in one
-// step of a part thread's loop the block's threads read nparts consecutive
-// rows (nparts * F floats, coalesced), and the second pass re-reads them from
-// the caches.  Without the 256 x F tile 4 blocks fit a CU at any F (the tile
-// allowed 2 at F = 50); loads go out 8 per thread at a time.
-__global__ void __launch_bounds__(256) col_stats_rows_kernel(const float* __restrict__ X, int F,
+// read straight from global memory into registers instead of through an
+// LDS tile: at each of a part thread's rows the block's threads read nparts
+// consecutive rows (nparts * F floats, coalesced), and both passes read the
+// registers.  Without the 256 x F tile 4 blocks fit a CU at any F (the tile
+// allowed 2 at F = 50).
+__global__ void __launch_bounds__(256, 4) col_stats_rows_kernel(const float* __restrict__ X, int F,
                                                              int64_t S, int64_t R,
                                                              double* __restrict__ rec) {
   __shared__ double s_st[4 * 256];
@@ -601,49 +601,49 @@ __global__ void __launch_bounds__(256) col_stats_rows_kernel(const float* __rest
   double n_acc = 0.0, m_acc = 0.0, q_acc = 0.0;
   float a_acc = 0.0f;
   const int64_t lo = (int64_t)blockIdx.x * R, hi = min(S, lo + R);
-  constexpr int kB = 8;
+  // a part thread's rows of one tile (spart, spart + nparts, ...: at most
+  // 64 for F <= 64) are loaded together into registers, then both passes
+  // run from them: one memory round trip per tile instead of one per batch
+  constexpr int kRows = 64;
   if (st_on) {
     for (int64_t r0 = lo; r0 < hi; r0 += kTile) {
       const int nrow = (int)min((int64_t)kTile, hi - r0);
-      const float* __restrict__ xc = X + r0 * F + sf;
-      const int64_t step = (int64_t)nparts * F;
+      // buffer loads: per-lane offset of the thread's first row, the row
+      // steps as scalar offsets (no 64-bit address per load); past the
+      // array's end they return 0 (unused: the passes skip rows >= nrow)
+      const uint64_t nb = (uint64_t)(S - r0) * F * 4;
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(X + r0 * F), (short)0, (int)(uint32_t)(nb < 0xFFFFFFFFull ? nb : 0xFFFFFFFFull),
+          0x00020000);
+      const int voff = (spart * F + sf) * 4, step4 = nparts * F * 4;
+      float v[kRows];
+#pragma unroll
+      for (int i = 0; i < kRows; ++i)
+        v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, voff, i * step4, 0));
+      // this thread's rows in the tile (rows spart + i * nparts < nrow)
+      int nmine = nrow > spart ? (nrow - spart + nparts - 1) / nparts : 0;
       double s = 0.0, cnt = 0.0;
-      int r = spart;
-      for (; r + (kB - 1) * nparts < nrow; r += kB * nparts) {
-        float v[kB];
 #pragma unroll
-        for (int i = 0; i < kB; ++i) v[i] = xc[(int64_t)r * F + i * step];
-#pragma unroll
-        for (int i = 0; i < kB; ++i) {
+      for (int i = 0; i < kRows; ++i)
+        if (i < nmine) {
           s += (double)v[i];
           cnt += 1.0;
           a_acc = fmaxf(a_acc, fabsf(v[i]));
         }
-      }
-      for (; r < nrow; r += nparts) {
-        const float v = xc[(int64_t)r * F];
-        s += (double)v;
-        cnt += 1.0;
-        a_acc = fmaxf(a_acc, fabsf(v));
-      }
+      // (opaque to the compiler: pass 2 converts again instead of keeping 64
+      // fp64 copies live across the division)
+#pragma unroll
+      for (int i = 0; i < kRows; ++i) asm volatile("" : "+v"(v[i]));
+      asm volatile("" : "+v"(nmine));
       if (cnt > 0.0) {
         const double m = s / cnt;
         double q = 0.0;
-        r = spart;
-        for (; r + (kB - 1) * nparts < nrow; r += kB * nparts) {
-          float v[kB];
 #pragma unroll
-          for (int i = 0; i < kB; ++i) v[i] = xc[(int64_t)r * F + i * step];
-#pragma unroll
-          for (int i = 0; i < kB; ++i) {
+        for (int i = 0; i < kRows; ++i)
+          if (i < nmine) {
             const double d = (double)v[i] - m;
             q += d * d;
           }
-        }
-        for (; r < nrow; r += nparts) {
-          const double d = (double)xc[(int64_t)r * F] - m;
-          q += d * d;
-        }
         chan_merge(n_acc, m_acc, q_acc, cnt, m, q);
       }
     }
