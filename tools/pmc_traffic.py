@@ -36,13 +36,16 @@ KERNELS = {
     "lloyd_tile_f64": "lloyd_pass_kernel<64, 0, 1, 1>",
     "lloyd_queue_f64": "lloyd_pass_kernel<64, 0, 2, 1>",
     "lloyd_final_f64": "lloyd_pass_kernel<64, 1, 0, 1>",
+    "lloyd_list_f64": "lloyd_pass_kernel<64, 0, 4, 1>",
+    "lloyd_list": "lloyd_pass_kernel<32, 0, 4, 1>",
+    "lloyd_mark": "lloyd_mark_kernel",
     "sample_map": "sample_map_kernel",
-    "col_stats": "gather_kernel<false>",
+    "col_stats": "col_stats_rows_kernel",
     "gather": "gather_kernel<true>",
     "nz_stats": "nz_stats_u16_kernel",
     "mask_scatter": "mask_scatter_kernel",
 }
-UNCALIBRATED = {"gather", "blur_sample", "sample_map"}  # random rows / atomics: not wide coalesced streams
+UNCALIBRATED = {"gather", "blur_sample", "sample_map", "lloyd_list", "lloyd_list_f64"}  # random rows / atomics: not wide coalesced streams
 
 
 def per_launch(path, pat):
