@@ -45,7 +45,8 @@ KERNELS = {
     "nz_stats": "nz_stats_u16_kernel",
     "mask_scatter": "mask_scatter_kernel",
 }
-UNCALIBRATED = {"gather", "blur_sample", "sample_map", "lloyd_list", "lloyd_list_f64"}  # random rows / atomics: not wide coalesced streams
+# not wide coalesced streams: random rows / atomics, and 4-byte loads (col_stats)
+UNCALIBRATED = {"gather", "blur_sample", "sample_map", "lloyd_list", "lloyd_list_f64", "col_stats"}
 
 
 def per_launch(path, pat):
