@@ -247,14 +247,42 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
 #pragma unroll
         for (int c = 0; c < T; ++c) dot[c] = fma(xs, q.c[c], dot[c]);
       };
-      TabF t0 = ld(0), t1 = ld(1);
-      for (int f = 0; f < fend; f += 2) {  // features past F add exact zeros
-        const TabF n0 = ld(f + 2), n1 = ld(f + 3);
-        const f2v x2 = *reinterpret_cast<const f2v*>(xr + f);
-        featt((double)x2.x, t0);
-        featt((double)x2.y, t1);
-        t0 = n0;
-        t1 = n1;
+#ifndef MW_KPP_SPIPE
+#define MW_KPP_SPIPE 64  // FMAX from which the pipelined form below is used
+#endif
+      if constexpr (FMAX >= MW_KPP_SPIPE) {
+        // the row's feature pairs into registers first (one LDS wait), then
+        // per pair: wait for the table loads issued one pair earlier (nothing
+        // else is outstanding on the shared LDS/scalar counter), issue the next
+        // pair's table loads, compute from registers only, so the scalar loads
+        // land under the FMAs instead of being waited for with each LDS read
+        f2v xrow[FMAX / 2];
+#pragma unroll
+        for (int p = 0; p < FMAX / 2; ++p)
+          xrow[p] = 2 * p < fend ? *reinterpret_cast<const f2v*>(xr + 2 * p) : f2v{0.f, 0.f};
+        TabF t0 = ld(0), t1 = ld(1);
+#pragma unroll
+        for (int p = 0; p < FMAX / 2; ++p) {
+          if (2 * p >= fend) break;  // features past F add exact zeros
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): t0, t1 (and the row reads) landed
+          const TabF n0 = ld(2 * p + 2), n1 = ld(2 * p + 3);
+          featt((double)xrow[p].x, t0);
+          featt((double)xrow[p].y, t1);
+          t0 = n0;
+          t1 = n1;
+        }
+        // (config-5 slice, F = 50: k-means++ 4 ms faster per slide at 2 waves
+        // per SIMD; at F <= 32 it measured neutral, the form below stays)
+      } else {
+        TabF t0 = ld(0), t1 = ld(1);
+        for (int f = 0; f < fend; f += 2) {  // features past F add exact zeros
+          const TabF n0 = ld(f + 2), n1 = ld(f + 3);
+          const f2v x2 = *reinterpret_cast<const f2v*>(xr + f);
+          featt((double)x2.x, t0);
+          featt((double)x2.y, t1);
+          t0 = n0;
+          t1 = n1;
+        }
       }
     } else {
 #pragma unroll 4
