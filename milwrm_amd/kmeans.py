@@ -393,45 +393,7 @@ def trace_summary(fits_hist=None):
     return out
 
 
-# Batched fits over rows of 17..31 features run on a copy padded to 32 (zero
-# columns, zero scaler): a 128-byte row is one whole cache line, so the list
-# pass's row gather reads one line per row instead of two for most rows, and
-# the E-step, M-step and inertia see the same fp32 chain (the kernels already
-# run 32 features with the padded pair exactly 0) -- identical results.
-# MW_LLOYD_PAD=1 turns it on (off by default until measured on the GPU).
-PAD_ROWS = os.environ.get("MW_LLOYD_PAD", "0") == "1"
-
-
-def _padded_rows(rows: DeviceRows, comm):
-    """The rows with zero columns up to 32 features (or None when they do not
-    need or fit it)."""
-    S, F = rows.S, rows.F
-    if not (17 <= F <= 31) or S == 0 or (comm is not None and comm.sharded()):
-        return None  # (sharded: every rank would have to take the same decision)
-    dev = rows.X.device
-    free, _ = torch.cuda.mem_get_info(dev)
-    if S * 32 * 4 * 2 > free:
-        return None
-    rows.fixed_point(comm)  # the column maxima (all shards) of the real features
-    z = np.zeros(32 - F)
-    Xp = torch.zeros((S, 32), dtype=torch.float32, device=dev)
-    Xp[:, :F] = rows.X
-    return DeviceRows(Xp, np.concatenate([rows.mu, z]), np.concatenate([rows.inv, z]),
-                      xmax_local=np.concatenate([rows.xmax.astype(np.float64), z]))
-
-
 def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, comm=LOCAL):
-    if PAD_ROWS and len(inits) > 1:
-        rows_p = _padded_rows(rows, comm)
-        if rows_p is not None:
-            F, Fp = rows.F, rows_p.F
-            inits_p = [np.pad(np.asarray(c, dtype=np.float64), ((0, 0), (0, Fp - F))) for c in inits]
-            out = _lloyd_fits(rows_p, inits_p, max_iter, tol, verbose, comm)
-            return [(lab, inertia, np.ascontiguousarray(c[:, :F]), n) for lab, inertia, c, n in out]
-    return _lloyd_fits(rows, inits, max_iter, tol, verbose, comm)
-
-
-def _lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, comm=LOCAL):
     """``_kmeans_single_lloyd`` (_kmeans.py:624-752) for one or several
     independent fits over the same rows, run in lockstep: every iteration is
     ONE mw_lloyd_pass for all the fits still running (up to 24 per launch),
