@@ -144,3 +144,15 @@ def test_mt_jump_tables_and_host_jump_match_sequential_stream():
         ref = wins[(L << j) // 624]
         np.testing.assert_array_equal(out[1:], ref[1:])
         assert (out[0] >> 31) == (ref[0] >> 31)
+
+
+def test_lloyd_workspace_holds_records_and_row_lists():
+    """mw_lloyd_ws_bytes covers the per-block records plus the kList pass's
+    per-block lengths and row lists (at least 4 bytes per row): callers that
+    size the workspace from the query get the list pass without changes."""
+    from milwrm_amd import _native as N
+
+    for S, k, F in [(1, 1, 1), (1000, 8, 30), (17_000_000, 20, 30), (270_000_000, 8, 50)]:
+        ws = N.query("mw_lloyd_ws_bytes", S, k, F)
+        rec = N.query("mw_lloyd_rec_len", k, F) * 8
+        assert ws >= rec + 4 * S, (S, k, F, ws)
