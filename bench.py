@@ -36,14 +36,20 @@ METRIC = "pixels/sec (node) for preprocess+k-means fit+label, 30-ch MxIF k=8; %H
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); measured copy ceiling ~6300
 
 
-def _config_name(H, W, C):
-    """Which BASELINE.json config one GPU's slice of this workload is."""
-    if (H, W, C) == (10000, 10000, 30):
+def _config_name(H, W, C, n, world, sweep=False):
+    """Which BASELINE.json config this workload is (``n`` slides per GPU)."""
+    if sweep:
+        if (H, W, C) == (20000, 20000, 30) and n == 1:
+            return "BASELINE config 4: the k=2..20 sweep over config 3's slides (one 20k^2 x 30 slide per GPU)"
+        return "find_optimal_k sweep k=2..20 (config 4 shape) over custom slides"
+    if (H, W, C) == (10000, 10000, 30) and n == 1:
         return "BASELINE config 2 per GPU"
-    if (H, W, C) == (20000, 20000, 30):
+    if (H, W, C) == (20000, 20000, 30) and n == 1:
         return "BASELINE config 3 per GPU: one of its 8 slides"
     if (H, W, C) == (40000, 40000, 50):
-        return "BASELINE config 5 per GPU: one of its 16 slides (one slide per GPU step)"
+        if n * world == 16:
+            return f"BASELINE config 5: its 16-slide cohort, {n} slides per GPU"
+        return f"BASELINE config 5 per GPU: {n} of its 16 slides per GPU"
     return "custom size"
 
 
@@ -56,12 +62,63 @@ def parse():
     ap.add_argument("--channels", type=int, default=30)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--mode", default="hard", choices=["hard", "easy"])
+    ap.add_argument("--slides-per-gpu", type=int, default=1,
+                    help="slides each rank labels per step (config 5: 2 on 8 GPUs)")
+    ap.add_argument("--source", default="auto", choices=["auto", "device", "synth", "host"],
+                    help="where the raw slides live: device = resident in HBM before the timed "
+                         "region; synth = not resident, generated band by band on the device "
+                         "inside the step (the stand-in for a slide reader); host = pinned host "
+                         "memory, streamed / uploaded by the residency policy inside the step; "
+                         "auto = device when all fit in 60%% of HBM, else synth")
+    ap.add_argument("--sweep", action="store_true",
+                    help="time find_optimal_k (k=2..20) over the prepped rows instead of the "
+                         "label pipeline (BASELINE config 4)")
     ap.add_argument("--cpu-size", type=int, default=2048, help="oracle CPU-baseline slide side")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
 
-def make_step(raw, mask, k, comm):
+class Slides:
+    """The raw slides of this rank, kept where ``--source`` puts them; ``img``
+    objects are made fresh for every step."""
+
+    def __init__(self, H, W, C, seeds, source, mode):
+        import milwrm_amd as M
+        from milwrm_amd import device as D
+        from milwrm_amd import stream
+
+        self.M, self.stream = M, stream
+        self.source = source
+        self.items = []
+        for seed in seeds:
+            if source == "device":
+                self.items.append(D.synth_slide(H, W, C, seed=seed, mode=mode))
+            elif source == "synth":
+                self.items.append(stream.SynthSource(H, W, C, seed, mode))
+            else:  # host: generated band by band on the device into pinned host memory
+                src = stream.SynthSource(H, W, C, seed, mode)
+                host = stream.pinned_empty((H, W, C), torch.int16)
+                rows = max(1, (1 << 30) // (W * C * 2))
+                buf = torch.empty((rows, W, C), dtype=torch.int16, device="cuda")
+                for y0 in range(0, H, rows):
+                    y1 = min(H, y0 + rows)
+                    src.read(y0, y1, buf)
+                    host[y0:y1].copy_(buf[:y1 - y0])
+                del buf
+                mask = src.mask_device().cpu().numpy()
+                self.items.append((host.numpy().view(np.uint16), mask))
+        torch.cuda.synchronize()
+
+    def images(self):
+        M = self.M
+        if self.source == "device":
+            return [M.img.from_device(raw, mask) for raw, mask in self.items]
+        if self.source == "synth":
+            return [M.img.from_source(src) for src in self.items]
+        return [M.img(a, mask=m) for a, m in self.items]
+
+
+def make_step(slides, C, k, comm, sweep=False):
     import pandas as pd
 
     import milwrm_amd as M
@@ -70,34 +127,70 @@ def make_step(raw, mask, k, comm):
         with contextlib.redirect_stdout(sys.stderr):  # reference-style progress prints
             return _step()
 
-    def _step():
-        im = M.img.from_device(raw, mask)
-        est, pix = im.calculate_non_zero_mean()
-        est, pix = comm.batch_stats(est, pix)
-        df = pd.DataFrame({"Img": [im], "batch_names": ["b"], "mean estimators": [est],
-                           "pixels": [pix]})
+    def prep():
+        ims = slides.images()
+        ests, pix = zip(*[im.calculate_non_zero_mean() for im in ims])
+        # one batch over every slide of every rank (mxif_labeler sums the
+        # estimators per batch over its images and, sharded, over the ranks)
+        df = pd.DataFrame({"Img": ims, "batch_names": ["b"] * len(ims),
+                           "mean estimators": list(ests), "pixels": list(pix)})
         lab = M.mxif_labeler(df)
-        lab.prep_cluster_data(features=list(range(raw.shape[2])), sigma=2, fract=0.2,
-                              comm=comm)
+        lab.prep_cluster_data(features=list(range(C)), sigma=2, fract=0.2, comm=comm)
+        return lab
+
+    def _step():
+        lab = prep()
         lab.label_tissue_regions(k=k, plot_out=False, random_state=18, comm=comm)
         lab.confidence_score_images()
         return lab
 
-    return step
+    if not sweep:
+        return step
+    state = {}
+
+    def sweep_step():
+        # the rows are prepped once (the first, untimed warmup call); each
+        # step is the whole find_optimal_k over them
+        if "lab" not in state:
+            with contextlib.redirect_stdout(sys.stderr):
+                state["lab"] = prep()
+        lab = state["lab"]
+        with contextlib.redirect_stdout(sys.stderr):
+            lab.find_optimal_k(random_state=18, alpha=0.05)
+        return lab
+
+    return sweep_step
 
 
-def cpu_baseline(size, C, k):
+def cpu_baseline(size, C, k, sweep=False):
     """Oracle (numpy/scipy restatement of the reference pipeline) on a bounded
-    host sample; Mpix/s on this box's cores."""
+    host sample; pixels/s on this box's cores.  ``sweep``: the oracle's
+    find_optimal_k (19 sklearn-restated fits) over the rows of a smaller
+    slide (prep untimed)."""
     from threadpoolctl import threadpool_info
 
     from oracle import milwrm_oracle as O
 
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    if sweep:
+        size = min(size, 512)
+        raw, mask = O.synth_slide(size, size, C, seed=20251015, mode="hard")
+        est, pix = O.non_zero_mean(raw)
+        mean = np.asarray(est) / pix
+        X, _ = O.subsample_pixels(O.gaussian_blur(O.log_normalize(raw, mean)), mask, list(range(C)))
+        mu, sc, _ = O.scaler_fit(X)
+        Xs = O.scaler_transform(X, mu, sc)
+        t = time.perf_counter()
+        best = O.choose_best_k(Xs)
+        dt = time.perf_counter() - t
+        return dict(value=size * size / dt, unit="pixels/s", cores=int(threads), kind="port",
+                    sample=f"oracle choose_best_k (k=2..20) over the {Xs.shape[0]} rows of one "
+                           f"{size}x{size}x{C} synthetic slide (best_k {best[0]}), {dt:.1f} s, "
+                           f"numpy/OpenBLAS threads={threads}")
     raw, mask = O.synth_slide(size, size, C, seed=20251015, mode="hard")
     t = time.perf_counter()
     r = O.mxif_pipeline([raw], [mask], ["b"], list(range(C)), k=k)
     dt = time.perf_counter() - t
-    threads = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
     return dict(value=size * size / dt, unit="pixels/s", cores=int(threads), kind="port",
                 sample=f"oracle mxif_pipeline on one {size}x{size}x{C} synthetic slide, k={k} "
                        f"(n_iter {r['kmeans']['n_iter_']}), {dt:.1f} s, numpy/OpenBLAS threads="
@@ -209,16 +302,21 @@ def main():
     comm = make_comm()
     H = W = args.size
     C = args.channels
-    raw, mask = D.synth_slide(H, W, C, seed=20251015 + rank, mode=args.mode)
-    torch.cuda.synchronize()
-    step = make_step(raw, mask, args.k, comm)
+    n_sl = args.slides_per_gpu
+    source = args.source
+    if source == "auto":
+        total = torch.cuda.get_device_properties(local).total_memory
+        source = "device" if n_sl * H * W * C * 2 <= 0.6 * total else "synth"
+    seeds = [20251015 + rank * n_sl + i for i in range(n_sl)]
+    slides = Slides(H, W, C, seeds, source, args.mode)
+    step = make_step(slides, C, args.k, comm, sweep=args.sweep)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1 if args.sweep else 0)):
         step()
     barrier()
     profiling.reset()
@@ -232,7 +330,8 @@ def main():
     t0 = time.perf_counter()
     lab = None
     for _ in range(args.steps):
-        lab = None  # the last step's buffers go before the next step allocates (40k^2 x 50 fits once)
+        if not args.sweep:
+            lab = None  # the last step's buffers go before the next step allocates (40k^2 x 50 fits once)
         lab = step()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -250,24 +349,31 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
-    px_total = world * H * W * args.steps
+    px_total = world * n_sl * H * W * args.steps
     value = px_total / elapsed
 
-    n_iter = int(lab.kmeans.n_iter_)
-    S = int(lab._rows.S)
-    # dominant kernel by device time inside the timed region
-    # (timed regions without an algorithmic byte count, e.g. the whole k-means
-    # fit in the C++ driver, are not kernels with a roofline)
-    dom_name, dom = max(((n, r) for n, r in prof.items() if r["bytes"] > 0),
+    S = int(lab._rows.S)  # this rank's rows (all its slides)
+    F, k = C, args.k
+    # dominant kernel by device time inside the timed region (timed regions
+    # without an algorithmic byte count, e.g. the whole k-means fit in the C++
+    # driver, are not kernels with a roofline; read_* is the slide reader)
+    dom_name, dom = max(((n, r) for n, r in prof.items() if r["bytes"] > 0 and not n.startswith("read_")),
                         key=lambda kv: kv[1]["total_ms"])
     per_launch_bytes = dom["bytes"] / max(dom["count"], 1)
     achieved = per_launch_bytes / (dom["mean_ms"] * 1e-3) / 1e9
     traffic, traffic_src, counters = pmc_traffic(dom_name, "_c5" if (H, W, C) == (40000, 40000, 50) else "")
-    # SURVEY §8(d) whole-pipeline algorithmic bytes (per slide)
-    N_pix, F, k = H * W, C, args.k
-    B = (N_pix * C * 2 + (N_pix * C * 2 + N_pix + S * F * 4) + (k + n_iter + 1) * S * F * 4
-         + (N_pix * F * 2 + N_pix + 5 * N_pix))
-    pipe_gbps = B * world / (elapsed / args.steps) / 1e9
+    reads = {n: r for n, r in prof.items() if n.startswith("read_")}
+    read_info = None
+    if reads:
+        rb = sum(r["bytes"] for r in reads.values()) / args.steps
+        rms = sum(r["total_ms"] for r in reads.values()) / args.steps
+        read_info = {"kind": source, "bytes_per_step": rb, "ms_per_step_side_stream": rms,
+                     "GBps": rb / max(rms, 1e-9) / 1e6,
+                     "note": "raw slide bands read on a side stream (overlapping the passes on the "
+                             "main stream) inside the timed step; synth = generated on the device, "
+                             "host = host-to-device copies over PCIe"}
+    workload = (f"mxif_labeler: {world} GPU(s) x {n_sl} synthetic {C}-ch {H}x{W} slide(s) per GPU, "
+                f"k={k}, sigma=2, fract=0.2, random_state=18 ({_config_name(H, W, C, n_sl, world, args.sweep)})")
     out = {
         "metric": METRIC,
         "value": value,
@@ -281,26 +387,53 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 (fp64 accumulation)",
         "data": "synthetic (device-generated Voronoi/gamma slides, SURVEY 8d; uint16 HWC + mask)",
-        "config": {"workload": f"mxif_labeler: {world} x synthetic {C}-ch {H}x{W} slide (one per GPU), "
-                               f"k={k}, sigma=2, fract=0.2, random_state=18 ({_config_name(H, W, C)})",
-                   "blur": "deferred (fused epilogues)" if D.defer_blur(H, W, C) else "materialised",
-                   "slides_per_gpu": 1, "H": H, "W": W, "C": C, "k": k, "mode": args.mode,
-                   "samples_per_slide": S, "lloyd_iters": n_iter, "parallelism": f"dp{world}"},
+        "config": {"workload": workload, "source": source,
+                   "blur": ("deferred (fused epilogues)" if source != "device" or D.defer_blur(H, W, C)
+                            else "materialised"),
+                   "slides_per_gpu": n_sl, "H": H, "W": W, "C": C, "k": k, "mode": args.mode,
+                   "samples_per_slide": S // n_sl, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "counters": counters,
                      "launches": dom["count"], "avg_launch_ms": dom["mean_ms"],
                      "algorithmic_bytes_per_launch": per_launch_bytes},
-        "pipeline_roofline": {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,
-                              "unit": "GB/s", "frac": pipe_gbps / (HBM_PEAK_GBPS * world)},
+        "slide_reads": read_info,
         "kernels": {n: {"count": v["count"], "mean_ms": round(v["mean_ms"], 4),
                         "total_ms_per_step": round(v["total_ms"] / args.steps, 4)}
                     for n, v in sorted(prof.items())},
         "cpu_baseline": None,
     }
+    if args.sweep:
+        curve = lab.inertia_curve_
+        iters = curve.attrs.get("n_iter", {})
+        passes = [n for n in prof if n.startswith("lloyd_pass") or n.startswith("lloyd_mark")]
+        pass_ms = sum(prof[n]["total_ms"] for n in passes) / args.steps
+        fit_passes = sum(int(v) + 1 for v in iters.values())  # Lloyd iterations + the final E-step
+        S_glob = S * world
+        out["metric"] = ("pixels/sec (node) through find_optimal_k (k=2..20 sweep, inertia curve) over "
+                         "the prepped rows of 30-ch MxIF slides")
+        out["sweep"] = {"seconds": ms / 1e3, "best_k": int(lab.k), "rows_total": S_glob,
+                        "n_iter": {int(a): int(b) for a, b in iters.items()},
+                        "fit_passes": fit_passes, "lloyd_device_ms": pass_ms,
+                        "device_ms_per_fit_pass": pass_ms / max(fit_passes, 1),
+                        "curve": [float(v) for v in curve["Scaled Inertia"].values]}
+        out["config"]["workload"] = (f"find_optimal_k k=2..20 over {world} GPU(s) x {n_sl} synthetic "
+                                     f"{C}-ch {H}x{W} slide(s) per GPU ({S_glob} rows; "
+                                     f"{_config_name(H, W, C, n_sl, world, True)})")
+    else:
+        n_iter = int(lab.kmeans.n_iter_)
+        # SURVEY §8(d) whole-pipeline algorithmic bytes (per slide)
+        N_pix = H * W
+        S1 = S / n_sl
+        B = (N_pix * C * 2 + (N_pix * C * 2 + N_pix + S1 * F * 4) + (k + n_iter + 1) * S1 * F * 4
+             + (N_pix * F * 2 + N_pix + 5 * N_pix))
+        pipe_gbps = B * world * n_sl / (elapsed / args.steps) / 1e9
+        out["config"]["lloyd_iters"] = n_iter
+        out["pipeline_roofline"] = {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,
+                                    "unit": "GB/s", "frac": pipe_gbps / (HBM_PEAK_GBPS * world)}
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_size, C, args.k)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_size, C, args.k, sweep=args.sweep)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -130,6 +130,22 @@ int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const floa
                    int64_t S, const int32_t* d_feat, int F, float* d_X, void* stream);
 int mw_sample_overflow(const int32_t* d_idx, const uint32_t* d_rank2pix, const int32_t* d_slots,
                        const int32_t* d_ovf, int64_t S, int F, float* d_X, void* stream);
+/* Row-window form for a slide streamed in row bands (img.subsample_pixels over a
+ * slide that is not resident in HBM, MxIF.py:457-492): d_img holds the H rows
+ * [row_off, row_off + H) of the slide (a band and its +-radius halo rows);
+ * only its rows [r0, r1) are blurred into samples, d_slots is the whole
+ * slide's table (indexed by slide pixel).  Calling it for bands that tile the
+ * slide writes exactly the rows of one mw_blur_sample over the whole slide. */
+int mw_blur_sample_rows(const void* d_img, int dtype, int H, int W, int C, int64_t row_off, int r0, int r1,
+                        const float* d_inv_mean, float pseudoval, const float* h_weights, int radius,
+                        const int32_t* d_slots, int64_t S, const int32_t* d_feat, int F, float* d_X,
+                        void* stream);
+/* The same rows from a band already blurred into fp32 (any shape the fused
+ * kernel does not take): d_band = n_pix HWC fp32 pixels, slide pixels
+ * [pix_off, pix_off + n_pix); X[j] = band[p - pix_off, feat] for both table
+ * slots j of every sampled pixel p of the band. */
+int mw_slot_gather(const float* d_band, int C, int64_t n_pix, int64_t pix_off, const int32_t* d_slots,
+                   int64_t S, const int32_t* d_feat, int F, float* d_X, void* stream);
 
 /* Chan-merge the per-block stats of the last gather(s) into d_stats =
  * [n, mean[F], M2[F]] (fp64).  `n_parts` gathers may be accumulated: pass
@@ -323,6 +339,13 @@ int mw_blur_assign_conf(const void* d_img, int dtype, int H, int W, int C, const
                         float pseudoval, const float* h_weights, int radius, const float* d_a,
                         const float* d_b, const float* d_centers, int k, const uint8_t* d_mask,
                         int8_t* d_label, float* d_conf, void* stream);
+/* Row-window form (a streamed slide band, as mw_blur_sample_rows): d_img
+ * holds slide rows [row_off, row_off + H); rows [r0, r1) are labelled;
+ * d_mask, d_label and d_conf are indexed by slide pixel. */
+int mw_blur_assign_rows(const void* d_img, int dtype, int H, int W, int C, int64_t row_off, int r0, int r1,
+                        const float* d_inv_mean, float pseudoval, const float* h_weights, int radius,
+                        const float* d_a, const float* d_b, const float* d_centers, int k,
+                        const uint8_t* d_mask, int8_t* d_label, float* d_conf, void* stream);
 int mw_domain_records(const int8_t* d_label, const float* d_conf, int64_t n_pix, int C, int k,
                       void* d_ws, void* stream);
 int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom,
@@ -379,6 +402,13 @@ int mw_synth_slide(int H, int W, int C, const float* d_seed_yx, int n_seeds,
                    const float* d_profiles, int n_domains, int shape_k,
                    int bg_rows, uint64_t seed, uint16_t* d_img, uint8_t* d_mask,
                    void* stream);
+/* Rows [y0, y1) of the same H x W slide into d_img ((y1-y0) x W x C) and, when
+ * d_mask != NULL, d_mask ((y1-y0) x W): bit for bit those rows of
+ * mw_synth_slide (every value is a hash of its slide pixel index).  The
+ * stand-in for reading a slide band from storage in the streamed benchmark. */
+int mw_synth_rows(int H, int W, int C, int y0, int y1, const float* d_seed_yx, int n_seeds,
+                  const float* d_profiles, int n_domains, int shape_k, int bg_rows, uint64_t seed,
+                  uint16_t* d_img, uint8_t* d_mask, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
 from .dist import LOCAL_COMM
-from .rng import check_total, set_global_state_after_draws, subsample_indices_device
+from .rng import _release_last_draw, check_total, set_global_state_after_draws, subsample_indices_device
 
 
 # ------------------------------------------------------------ k selection
@@ -63,8 +63,11 @@ def chooseBestKforKMeansParallel(scaled_data, k_range, n_jobs=-1, comm=None, **k
         fits = fit_many(rows, list(k_range), random_state=kwargs.get("random_state", 18),
                         comm=comm)
         ans = [km.inertia_ / inertia_o + alpha_k * k for km, k in zip(fits, k_range)]
+        n_iter = {int(k): int(km.n_iter_) for km, k in zip(fits, k_range)}
     ans = list(zip(k_range, ans))
     results = pd.DataFrame(ans, columns=["k", "Scaled Inertia"]).set_index("k")
+    if os.environ.get("MW_SWEEP_BATCH", "1") != "0":
+        results.attrs["n_iter"] = n_iter  # Lloyd iterations per k (bench.py --sweep)
     best_k = results.idxmin().iloc[0]
     return best_k, results
 
@@ -156,8 +159,8 @@ def _domain_stats(image, use_path, scaler, centroids, features, tissue_ID):
         # materialised slide's result
         sigma, truncate = image._pending_blur
         inv_mean, p = image._pending
-        return domain_sse_deferred(image._device(), sigma, inv_mean, p, feats, mu, inv, centroids,
-                                   tissue_ID, truncate=truncate)
+        return domain_sse_deferred(image._source() or image._device(), sigma, inv_mean, p, feats, mu,
+                                   inv, centroids, tissue_ID, truncate=truncate)
     return domain_sse_image(D.as_float32(image._materialize()), feats, mu, inv, centroids, tissue_ID)
 
 
@@ -220,9 +223,10 @@ def _check_rows_fit(S: int, F: int, dev) -> None:
     bounds, labels).  A cohort whose sampled rows exceed what is free (config
     5 at 1-2 GPUs: 870 GB of rows) raises here, before any allocation, with the
     remedy, instead of failing inside a kernel launch."""
+    from .stream import RESIDENCY
+
     need = S * (F * 4 + 17)
-    free, _ = torch.cuda.mem_get_info(dev)
-    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)  # torch's cache
+    free = RESIDENCY.release(need)  # resident copies of host-backed slides go first (stream.py)
     if need > free:
         raise MemoryError(
             f"the {S} clustering rows of this rank ({F} features) need {need / 2**30:.1f} GiB of HBM "
@@ -246,12 +250,18 @@ def _assign_img(image: img, features, centers, scaler):
         res = None
         band = getattr(image, "_band", None)  # a slide band: label its own rows only
         out_rows = None if band is None else (band.rows.start, band.rows.stop)
-        if how != "fused" or band is not None:
-            res = banded_assign_image(image._device(), sigma, inv_mean, p, feats, mu, inv, centers,
+        # resident raw slide, or (not resident) its stream.RowSource read band by band
+        raw = image._source() or image._device()
+        fusable = band is None and feats == list(range(image.n_ch))
+        if how == "fused" and fusable:
+            res = blur_assign_image(raw, sigma, inv_mean, p, mu, inv, centers, image._mask_device(),
+                                    truncate=truncate)
+        if res is None:
+            res = banded_assign_image(raw, sigma, inv_mean, p, feats, mu, inv, centers,
                                       image._mask_device(), truncate=truncate, out_rows=out_rows)
-        if res is None and band is None and feats == list(range(image.n_ch)):
-            res = blur_assign_image(image._device(), sigma, inv_mean, p, mu, inv, centers,
-                                    image._mask_device(), truncate=truncate)
+        if res is None and how != "fused" and fusable:  # not even a 16-row fp32 band fits
+            res = blur_assign_image(raw, sigma, inv_mean, p, mu, inv, centers, image._mask_device(),
+                                    truncate=truncate)
         if res is not None:
             return res
     src = D.as_float32(image._materialize())
@@ -266,12 +276,15 @@ def _gather_deferred(image: img, feat, idx, r2p, X_out) -> bool:
     """Subsample rows written by the blur itself for an image whose blur is
     deferred (D.defer_blur); False when it is not, or the fused kernel does
     not take the shape (the caller materialises and gathers)."""
+    from .stream import blur_gather
+
     if image._pending_blur is None:
         return False
     sigma, truncate = image._pending_blur
     inv_mean, p = image._pending
-    return D.blur_gather_fused(image._device(), sigma, inv_mean, p, feat, idx, r2p, X_out,
-                               truncate=truncate)
+    # resident raw slide (one band), or its stream.RowSource read band by band
+    return blur_gather(image._source() or image._device(), sigma, inv_mean, p, feat, idx, r2p, X_out,
+                       truncate=truncate)
 
 
 def _labels_to_host(lab: torch.Tensor) -> np.ndarray:
@@ -495,9 +508,15 @@ class mxif_labeler(tissue_labeler):
         if images:
             images[0].log_normalize(mean=means[batches[0]])
             images[0].blurring(filter_name=filter_name, sigma=sigma)
-        # phase 1: mask ranks → sample counts → one preallocated row block
+        # phase 1: mask ranks → sample counts → one preallocated row block.
+        # Only the first image keeps its rank→pixel table (4 bytes per tissue
+        # pixel: 5.4 GB per 40k^2 slide); the others are ranked again when
+        # their rows are gathered, so a cohort holds one table at a time
         dev = D.device()
-        ranks = [im._mask_rank() for im in images]
+        ranks = []
+        for i, im in enumerate(images):
+            r2p, M = im._mask_rank()
+            ranks.append((r2p if i == 0 else None, M))
         counts = [int(M * fract) for _, M in ranks]
         F = len(images[0]._features(features))
         _check_rows_fit(sum(counts), F, dev)
@@ -518,6 +537,8 @@ class mxif_labeler(tissue_labeler):
                 im.blurring(filter_name=filter_name, sigma=sigma)
             np.random.seed(16)
             if S:
+                if r2p is None:
+                    r2p, _ = im._mask_rank()
                 idx, tot = subsample_indices_device(M, fract, 16, dev)
                 totals.append((tot, S))
                 feat = D.h2d(np.asarray(im._features(features), dtype=np.int32), dev)
@@ -527,6 +548,13 @@ class mxif_labeler(tissue_labeler):
                 else:
                     D.gather_rows(D.as_float32(im._materialize()), feat, idx, r2p, X[off:off + S],
                                   img_stats[n_img], accumulate=False, absmax=xmax)
+                del idx
+            else:
+                # seed(16) then choice(M, 0) draws nothing: the global state
+                # is the fresh seed's, not past an earlier image's draws
+                _release_last_draw()
+            r2p = None
+            ranks[n_img] = (None, M)
             off += S
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))

@@ -78,19 +78,110 @@ class img:
         self.mask = mask
         self._mask_dev = None
         self._band = None  # bands.BandInfo when this img is one row band of a slide
+        self._src = None   # stream.RowSource of a slide that is read band by band
+        self._hsrc = None  # cached stream.HostSource over _host
+        self._revert = None  # how to redo a transformed copy (_transformed / _evict)
 
     # ----------------------------------------------------------- residency
+    # The raw pixels of a host-backed image are uploaded whole while they fit
+    # the HBM budget (stream.RESIDENCY, least recently used out); otherwise
+    # every pass that needs them streams them in row bands (milwrm_amd.stream)
     @property
     def shape(self):
-        return self._host.shape if self._dev is None else (
-            tuple(self._dev.shape) if self._ndim > 2 else tuple(self._dev.shape[:2]))
+        if self._dev is not None:
+            return tuple(self._dev.shape) if self._ndim > 2 else tuple(self._dev.shape[:2])
+        if self._host is None and self._src is not None:
+            return self._src.shape if self._ndim > 2 else self._src.shape[:2]
+        return self._host.shape
+
+    def _raw_nbytes(self) -> int:
+        from .stream import device_dtype_of
+
+        a = self._host
+        memo = getattr(self, "_rawb", None)
+        if memo is None or memo[0] is not a:
+            elem = torch.empty(0, dtype=device_dtype_of(a)).element_size()
+            memo = self._rawb = (a, int(a.size) * elem)
+        return memo[1]
 
     def _device(self) -> torch.Tensor:
-        """HWC device tensor (uploads on first use)."""
+        """HWC device tensor (uploads on first use; a host-backed upload may
+        first evict older resident copies, stream.RESIDENCY)."""
+        from .stream import RESIDENCY
+
         if self._dev is None:
-            a = self._host if self._host.ndim > 2 else self._host[:, :, None]
-            self._dev = D.to_device_image(a)
+            if self._host is None and self._src is not None:
+                self._dev = self._src.materialize()  # an explicit whole-slide read
+            else:
+                a = self._host if self._host.ndim > 2 else self._host[:, :, None]
+                RESIDENCY.admit(self, self._raw_nbytes())
+                self._dev = D.to_device_image(a)
+            RESIDENCY.register(self, self._dev.numel() * self._dev.element_size())
+        else:
+            RESIDENCY.touch(self)
         return self._dev
+
+    def _source(self):
+        """None when the raw pixels are resident (or are admitted now: the
+        caller then takes ``_device()``); else the ``stream.RowSource`` to read
+        them from band by band."""
+        from .stream import RESIDENCY, HostSource
+
+        if self._dev is not None:
+            RESIDENCY.touch(self)
+            return None
+        if self._band is not None:  # a slide band (milwrm_amd.bands) stays resident
+            return None
+        if self._host is None:
+            return self._src
+        if RESIDENCY.admit(self, self._raw_nbytes()):
+            return None
+        if self._hsrc is None:
+            self._hsrc = HostSource(self._host)
+        return self._hsrc
+
+    def _may_hold(self, nbytes: int) -> bool:
+        """Whether a device copy of ``nbytes`` may be kept for this image: any
+        for an image born on the device; within the HBM budget (evicting older
+        copies) for one a host array or a source backs."""
+        from .stream import RESIDENCY
+
+        if self._host is None and self._src is None:
+            return True
+        return RESIDENCY.admit(self, nbytes)
+
+    @classmethod
+    def from_source(cls, src, mask=None, channels=None) -> "img":
+        """An image whose raw pixels come from a ``stream.RowSource`` band by
+        band (never resident whole): a slide reader, a host array, or the
+        benchmark's synthetic generator.  ``mask``: host or device H x W
+        (default: the source's own mask)."""
+        obj = cls.__new__(cls)
+        obj._ndim = 3
+        obj._host = None
+        obj._host64 = None
+        obj._dev = None
+        obj._pending = None
+        obj._pending_blur = None
+        obj._src = src
+        obj._hsrc = None
+        obj._revert = None
+        obj.n_ch = int(src.C)
+        obj.ch = channels if channels is not None else ["ch_{}".format(x) for x in range(obj.n_ch)]
+        obj._mask = None
+        obj._mask_dev = None
+        obj._mrank = None
+        obj._band = None
+        if mask is None:
+            mask = src.mask_device()
+        if isinstance(mask, torch.Tensor):
+            obj._mask = _DeviceMask(mask)
+            obj._mask_dev = D.padded_mask((mask != 0).to(torch.uint8) if mask.dtype != torch.uint8 else mask)
+        elif mask is not None:
+            assert tuple(mask.shape) == (src.H, src.W), \
+                "Shape of mask must match the first two dimensions of img_arr"
+            obj._mask = mask
+        return obj
 
     def _materialize(self) -> torch.Tensor:
         """Apply a deferred blur (with its log_normalize fused) or a deferred
@@ -98,27 +189,62 @@ class img:
         if self._pending_blur is not None:
             sigma, truncate = self._pending_blur
             inv, p = self._pending
-            self._pending_blur = None
-            self._pending = None
-            self._set_device(D.blur(self._device(), sigma, inv_mean=inv, pseudoval=p,
-                                    truncate=truncate))
+            self._transformed(lambda: D.blur(self._device(), sigma, inv_mean=inv, pseudoval=p,
+                                             truncate=truncate))
         if self._pending is not None:
             inv, p = self._pending
-            self._pending = None
-            self._dev = D.lognorm(self._device(), inv, p)
-            self._host64 = None
+            if inv is None:
+                self._pending = None
+            else:
+                self._transformed(lambda: D.lognorm(self._device(), inv, p))
         return self._device()
 
+    def _transformed(self, make):
+        """Replace the pixels by ``make()`` (the pending transforms applied).
+        An image backed by a host array or a source keeps how to redo it: its
+        transformed copy stays evictable (``_evict`` returns it to the
+        deferred state, which gives the same bits, stream.py)."""
+        from .stream import RESIDENCY
+
+        backed = self._host is not None or self._src is not None
+        state = (self._host, self._src, self._pending, self._pending_blur) if backed else None
+        out = make()
+        self._pending = None
+        self._pending_blur = None
+        self._set_device(out)
+        if state is not None:
+            self._revert = state
+            RESIDENCY.register(self, out.numel() * out.element_size())
+
     def _set_device(self, t: torch.Tensor):
+        """The image's pixels are now ``t`` (not a raw copy that could be read
+        again: not evictable unless ``_transformed`` records how to redo it)."""
+        from .stream import RESIDENCY
+
+        RESIDENCY.forget(self)
         self._dev = t
         self._host64 = None
         self._host = None
+        self._src = None
+        self._hsrc = None
+        self._revert = None
+
+    def _evict(self):
+        """Drop the device copy: the raw copy of a host array / source, or a
+        transformed copy back to its deferred state."""
+        rv = getattr(self, "_revert", None)
+        if rv is not None:
+            self._host, self._src, self._pending, self._pending_blur = rv
+            self._revert = None
+            self._host64 = None
+        self._dev = None
 
     @property
     def img(self) -> np.ndarray:
         """The reference's float64 HWC array (materialised from HBM on read)."""
         if self._host64 is None:
-            if self._dev is None and self._pending is None and self._pending_blur is None:
+            if (self._dev is None and self._host is not None and self._pending is None
+                    and self._pending_blur is None):
                 self._host64 = self._host.astype("float64")
             else:
                 t = self._materialize()
@@ -128,11 +254,16 @@ class img:
 
     @img.setter
     def img(self, value):
+        from .stream import RESIDENCY
+
         value = np.asarray(value)
+        RESIDENCY.forget(self)
         self._ndim = value.ndim
         self._host = value
         self._host64 = None
         self._dev = None
+        self._src = None
+        self._hsrc = None
         self._pending = None
         self._pending_blur = None
 
@@ -184,6 +315,7 @@ class img:
         new._host = None if self._host is None else self._host.copy()
         new._host64 = None if self._host64 is None else self._host64.copy()
         new._dev = None if self._dev is None else self._dev.clone()
+        new._hsrc = None
         new._mask = None if self._mask is None else self._mask.copy()
         new._mask_dev = None
         new._mrank = None
@@ -225,6 +357,9 @@ class img:
         obj._mask_dev = None
         obj._mrank = None
         obj._band = None
+        obj._src = None
+        obj._hsrc = None
+        obj._revert = None
         if mask is not None:
             obj._mask = _DeviceMask(mask)
             obj._mask_dev = (mask != 0).to(torch.uint8) if mask.dtype != torch.uint8 else mask
@@ -297,17 +432,29 @@ class img:
             if mode != "nearest" or kwargs:
                 raise NotImplementedError(f"gaussian options {dict(mode=mode, **kwargs)} "
                                           "(only mode='nearest' is implemented)")
+            if self._pending_blur is None and self._source() is not None:
+                # not resident: the blur runs inside every pass over the
+                # streamed bands (stream.blur_gather, the banded label pass)
+                self._pending_blur = (float(sigma), truncate)
+                if self._pending is None:
+                    self._pending = (None, 1.0)  # no log-normalise before this blur
+                self._host64 = None
+                return
             src = self._materialize() if self._pending_blur is not None else self._device()
-            if self._pending is not None and src.dim() == 3 and D.defer_blur(*src.shape):
+            if self._pending is not None and src.dim() == 3 and (
+                    D.defer_blur(*src.shape) or not self._may_hold(src.numel() * 4)):
                 # fused-epilogue mode: the subsample gather and the label pass
-                # recompute the blur from the raw slide (D.defer_blur)
+                # recompute the blur from the raw slide (D.defer_blur, or the
+                # fp32 copy of a host-backed slide would exceed the HBM budget)
                 self._pending_blur = (float(sigma), truncate)
                 self._host64 = None
                 return
-            inv, p = self._pending if self._pending is not None else (None, 1.0)
-            self._pending = None
-            out = D.blur(src, float(sigma), inv_mean=inv, pseudoval=p, truncate=truncate)
-            self._set_device(out)
+            self._pending_blur = (float(sigma), truncate)
+            if self._pending is None:
+                self._pending = (None, 1.0)
+            inv, p = self._pending
+            self._transformed(lambda: D.blur(src, float(sigma), inv_mean=inv, pseudoval=p,
+                                             truncate=truncate))
         elif filter_name == "median":
             # The reference's median branch calls np.ones(sigma, sigma), which
             # raises for any integer sigma (MxIF.py:403); keep that behaviour.
@@ -331,12 +478,11 @@ class img:
             print("WARNING: Performing normalization without a tissue mask.")
         if mean is None:
             print("mean calculated to perform log normalization")
-            src = self._materialize()
-            s, _ = D.nz_stats(src)  # zeros add nothing: channel sum over all pixels
-            n = src.shape[0] * src.shape[1]
+            s, _ = self._nz_stats()  # zeros add nothing: channel sum over all pixels
+            n = self.shape[0] * self.shape[1]
             mean = s.cpu().numpy() / n
-        else:
-            self._materialize()
+        elif self._pending is not None or self._pending_blur is not None:
+            self._materialize()  # a transform already pending applies first
         mean = np.asarray(mean, dtype=np.float64)
         with np.errstate(divide="ignore"):
             inv = (1.0 / mean).astype(np.float32)
@@ -347,11 +493,14 @@ class img:
                           accumulate=False):
         """Device subsample: mask rank → legacy-RNG indices → row gather into
         ``X_out`` (fp32) with column statistics folded into ``stats``."""
+        from .stream import blur_gather
+
         features = self._features(features)
         np.random.seed(random_state)  # the reference's global-RNG side effect (MxIF.py:484)
-        src = D.as_float32(self._materialize())
+        deferred = self._pending_blur is not None
+        src = None if deferred else D.as_float32(self._materialize())
         r2p, M = self._mask_rank()
-        dev = src.device
+        dev = D.device()
         d_idx, total = subsample_indices_device(M, fract, random_state, dev)
         S = d_idx.shape[0]
         if X_out is None:
@@ -360,7 +509,14 @@ class img:
             stats = torch.zeros(1 + 2 * len(features), dtype=torch.float64, device=dev)
         if S:
             feat = D.h2d(np.asarray(features, dtype=np.int32), dev)
-            D.gather_rows(src, feat, d_idx, r2p, X_out, stats, accumulate)
+            if deferred:  # rows straight from the blur (resident or streamed slide)
+                sigma, truncate = self._pending_blur
+                inv, p = self._pending
+                blur_gather(self._source() or self._device(), sigma, inv, p, feat, d_idx, r2p, X_out,
+                            truncate)
+                D.col_stats_rows(X_out, stats, accumulate)
+            else:
+                D.gather_rows(src, feat, d_idx, r2p, X_out, stats, accumulate)
             check_total(total, S)
             set_global_state_after_draws()
         return X_out, stats
@@ -381,6 +537,18 @@ class img:
         out = D.block_mean(self._materialize(), int(fact))
         self._set_device(out)
 
+    def _nz_stats(self):
+        """Per-channel non-zero (sum, count) of the current pixels: band by
+        band when the raw slide is not resident (stream.nz_stats: exact
+        integer sums for uint8 / uint16, the whole-slide bits)."""
+        from . import stream
+
+        src = self._source() if self._pending is None and self._pending_blur is None else None
+        if src is not None:
+            D.FUSED_USED["nz_streamed"] += 1
+            return stream.nz_stats(src)
+        return D.nz_stats(self._materialize())
+
     def calculate_non_zero_mean(self, comm=None):
         """MxIF.py:519-541: ([mean_c * pixels], pixels) with pixels = non-zero
         elements over all channels.  A row band of a slide (milwrm_amd.bands)
@@ -396,7 +564,7 @@ class img:
             with np.errstate(invalid="ignore", divide="ignore"):
                 means = s / c
             return [float(m) * pixels for m in means], pixels
-        s, c = D.nz_stats(self._materialize())
+        s, c = self._nz_stats()
         self._prefetch_mask_rank()  # queued behind nz_stats, overlaps the host work that follows
         s, c = D.d2h(s, c)
         pixels = int(c.sum())

@@ -88,6 +88,13 @@ _PROTOS = {
     "mw_blur_assign_conf": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mw_domain_records": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mw_synth_slide": (c_i32, [c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_u64, c_vp, c_vp, c_vp]),
+    "mw_synth_rows": (c_i32, [c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_i32, c_i32, c_u64,
+                              c_vp, c_vp, c_vp]),
+    "mw_blur_sample_rows": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i64, c_i32, c_i32, c_vp, c_f32, c_vp,
+                                    c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "mw_slot_gather": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "mw_blur_assign_rows": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i64, c_i32, c_i32, c_vp, c_f32, c_vp,
+                                    c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
 }
 
 EXPORTED = tuple(_PROTOS)

@@ -41,44 +41,71 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
     return lab, conf, dom
 
 
-def blur_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: float, mu, inv,
-                      centers: np.ndarray, mask_u8: torch.Tensor, truncate: float = 4.0):
-    """``assign_image(blur(lognorm(raw)), all channels, ...)`` in one pass over
-    the raw slide (the fused blur assign epilogue; the blurred slide is never
-    stored), then the same per-block domain records.  None when the fused
-    kernel does not take this shape (the caller materialises the blur)."""
-    H, W, C = raw.shape
+def blur_assign_image(raw, sigma: float, inv_mean, pseudoval: float, mu, inv,
+                      centers: np.ndarray, mask_u8: torch.Tensor, truncate: float = 4.0, band_rows=None):
+    """``assign_image(blur(lognorm(raw)), all channels, ...)`` with the label
+    pass as the blur's epilogue (the blurred slide is never stored), then the
+    same per-block domain records.  ``raw``: a resident slide (one launch) or
+    a ``stream.RowSource`` (one launch per band of output rows,
+    mw_blur_assign_rows, which is bit for bit the whole-slide launch).  None
+    when the fused kernel does not take this shape (the caller materialises
+    the blur)."""
+    from .stream import as_source, band_rows_for, bands
+
+    src = as_source(raw)
+    H, W, C = src.shape
     k, F = centers.shape
     if F != C or inv_mean is None:
         return None
-    dev = raw.device
-    a = D.h2d(np.asarray(inv, dtype=np.float64).astype(np.float32), dev)
-    b = D.h2d((-np.asarray(mu, dtype=np.float64) * np.asarray(inv, dtype=np.float64))
-              .astype(np.float32), dev)
-    c32 = D.h2d(np.asarray(centers, dtype=np.float32), dev)
+    dev = D.device()
+    a, b, c32 = D.h2d_many([np.asarray(inv, dtype=np.float64).astype(np.float32),
+                            (-np.asarray(mu, dtype=np.float64) * np.asarray(inv, dtype=np.float64))
+                            .astype(np.float32), np.asarray(centers, dtype=np.float32)], dev)
     w = D.gaussian_taps(sigma, truncate)
     r = (len(w) - 1) // 2
     n = H * W
     lab = torch.empty((H, W), dtype=torch.int8, device=dev)
     conf = torch.empty((H, W), dtype=torch.float32, device=dev)
     mask_u8 = D.padded_mask(mask_u8)
-    st = D.stream()
-    with profiling.timed("blur_assign", n * (C * raw.element_size() + 5)):
-        ok = N.try_call("mw_blur_assign_conf", D.P(raw), D.dtype_code(raw), H, W, C, D.P(inv_mean),
-                        float(pseudoval), w.ctypes.data, r, D.P(a), D.P(b), D.P(c32), k,
-                        D.P(mask_u8), D.P(lab), D.P(conf), st)
-    if not ok:
-        return None
+    if band_rows is None:
+        band_rows = H if src.zero_copy else band_rows_for(src)
+    elem = torch.empty(0, dtype=src.dtype).element_size()
+    for y0, y1, a0, rb in bands(src, band_rows, r):
+        with profiling.timed("blur_assign", (y1 - y0) * W * (C * elem + 5)):
+            ok = N.try_call("mw_blur_assign_rows", D.P(rb), D.dtype_code(rb), int(rb.shape[0]), W, C, a0,
+                            y0 - a0, y1 - a0, D.P(inv_mean), float(pseudoval), w.ctypes.data, r, D.P(a),
+                            D.P(b), D.P(c32), k, D.P(mask_u8), D.P(lab), D.P(conf), D.stream())
+        if not ok:  # shape-determined: decided by the first band
+            return None
     D.FUSED_USED["assign"] += 1
+    if not src.zero_copy:
+        D.FUSED_USED["assign_streamed"] += 1
     dom = torch.empty(2 * k, dtype=torch.float64, device=dev)
     ws = D.WS.get("assign", N.query("mw_assign_ws_bytes", n, k))
+    st = D.stream()
     with profiling.timed("domain_records", n * 5):
         N.call("mw_domain_records", D.P(lab), D.P(conf), n, C, k, D.P(ws), st)
     N.call("mw_assign_reduce", D.P(ws), n, k, D.P(dom), st)
     return lab, conf, dom
 
 
-def banded_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
+def _assign_band_rows(src, r, extra_per_row, band_rows):
+    """Output rows per band of the banded label / QC passes: ``band_rows``,
+    else ``MW_ASSIGN_BAND_ROWS``, else (resident slide) what half the free
+    HBM holds as fp32, (streamed slide) ``stream.band_rows_for``."""
+    from .stream import band_rows_for, free_bytes
+
+    if band_rows is not None:
+        return int(band_rows)
+    env = os.environ.get("MW_ASSIGN_BAND_ROWS")
+    if env:
+        return int(env)
+    if src.zero_copy:
+        return int(free_bytes() // 2 // extra_per_row) - 2 * r
+    return band_rows_for(src, extra_per_row)
+
+
+def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
                         inv, centers: np.ndarray, mask_u8: torch.Tensor, truncate: float = 4.0,
                         band_rows=None, out_rows=None):
     """``assign_image(blur(lognorm(raw)))`` for a slide whose fp32 blurred copy
@@ -87,40 +114,40 @@ def banded_assign_image(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: fl
     does not depend on the band, so labels and confidences are bitwise those
     of the whole-slide blur) into one reused buffer, and each band goes
     through the label pass.  The per-domain sums are added band after band.
-    None when not even a 16-row band fits in half the free HBM.  ``out_rows``
-    = (r0, r1): label only those rows of ``raw`` (a slide band's own rows
-    inside its halo'd array, milwrm_amd.bands); outputs are (r1 - r0) x W."""
-    H, W, C = raw.shape
+    ``raw``: a resident slide or a ``stream.RowSource`` (a slide that is not
+    resident: its bands are read as they are needed, the next one while this
+    one is labelled).  None when not even a 16-row band fits in half the
+    free HBM.  ``out_rows`` = (r0, r1): label only those rows of ``raw`` (a
+    slide band's own rows inside its halo'd array, milwrm_amd.bands); outputs
+    are (r1 - r0) x W."""
+    from .stream import as_source, bands
+
+    src = as_source(raw)
+    H, W, C = src.shape
     r0, r1 = (0, H) if out_rows is None else (int(out_rows[0]), int(out_rows[1]))
     k, F = centers.shape
     w = D.gaussian_taps(sigma, truncate)
     r = (len(w) - 1) // 2
     row_bytes = W * C * 4
-    if band_rows is None:
-        env = os.environ.get("MW_ASSIGN_BAND_ROWS")
-        if env:
-            band_rows = int(env)
-        else:
-            free, _ = torch.cuda.mem_get_info()
-            band_rows = int(free // 2 // row_bytes) - 2 * r
+    band_rows = _assign_band_rows(src, r, row_bytes, band_rows)
     if band_rows < 16:
         return None
     band_rows = min(band_rows, r1 - r0)
-    dev = raw.device
+    dev = D.device()
     lab = torch.empty((r1 - r0, W), dtype=torch.int8, device=dev)
     conf = torch.empty((r1 - r0, W), dtype=torch.float32, device=dev)
     dom = torch.zeros(2 * k, dtype=torch.float64, device=dev)
     buf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=dev)
-    for y0 in range(r0, r1, band_rows):
-        y1 = min(r1, y0 + band_rows)
-        a, b = max(0, y0 - r), min(H, y1 + r)
-        out = buf[:b - a]
-        D.blur(raw[a:b], sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
+    for y0, y1, a, rb in bands(src, band_rows, r, r0, r1):
+        out = buf[:rb.shape[0]]
+        D.blur(rb, sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
         _, _, d = assign_image(out[y0 - a:y1 - a], feat_idx, mu, inv, centers,
                                D.padded_mask(mask_u8[y0:y1].contiguous()),
                                out_lab=lab[y0 - r0:y1 - r0], out_conf=conf[y0 - r0:y1 - r0])
         dom += d
     D.FUSED_USED["assign_banded"] += 1
+    if not src.zero_copy:
+        D.FUSED_USED["assign_streamed"] += 1
     return lab, conf, dom
 
 
@@ -268,7 +295,7 @@ def _first_pixel_scaled(img_f32, feat, mu, inv) -> np.ndarray:
         inv, dtype=np.float64)
 
 
-def domain_sse_deferred(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
+def domain_sse_deferred(raw, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
                         inv, centers: np.ndarray, tissue_id, truncate: float = 4.0,
                         band_rows=None) -> dict:
     """``domain_sse_image(blur(lognorm(raw)), ...)`` for a slide whose fp32
@@ -276,32 +303,32 @@ def domain_sse_deferred(raw: torch.Tensor, sigma: float, inv_mean, pseudoval: fl
     materialised band by band (band + r halo rows of input) into one reused
     buffer, twice -- once for the column maxima that fix the fixed point,
     once for the sums.  The sums are exact, so the result is bitwise the
-    materialised slide's (tests/test_gpu_qc.py)."""
-    H, W, C = raw.shape
+    materialised slide's (tests/test_gpu_qc.py).  ``raw``: a resident slide
+    or a ``stream.RowSource`` (read band by band, twice)."""
+    from .stream import as_source
+    from .stream import bands as read_bands
+
+    src = as_source(raw)
+    H, W, C = src.shape
     k, F = centers.shape
     feat = _check_feats(feat_idx, F, C)
     w = D.gaussian_taps(sigma, truncate)
     r = (len(w) - 1) // 2
-    if band_rows is None:
-        env = os.environ.get("MW_ASSIGN_BAND_ROWS")
-        if env:
-            band_rows = int(env)
-        else:
-            free, _ = torch.cuda.mem_get_info()
-            band_rows = int(free // 2 // (W * C * 4)) - 2 * r
+    band_rows = _assign_band_rows(src, r, W * C * 4, band_rows)
     if band_rows < 1:
         raise MemoryError("not even one row band of the blurred slide fits in half the free HBM")
     band_rows = min(band_rows, H)
-    dev = raw.device
+    # exact limbs: every band adds < 2^43 per quantity, the fp64 sums stay exact below 2^53
+    if -(-H // band_rows) >= 1 << 10:
+        band_rows = -(-H // ((1 << 10) - 1))
+    dev = D.device()
     lab = _labels_i8(tissue_id, H * W, k, dev)
     buf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=dev)
 
     def bands():
-        for y0 in range(0, H, band_rows):
-            y1 = min(H, y0 + band_rows)
-            a, b = max(0, y0 - r), min(H, y1 + r)
-            out = buf[:b - a]
-            D.blur(raw[a:b], sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
+        for y0, y1, a, rb in read_bands(src, band_rows, r):
+            out = buf[:rb.shape[0]]
+            D.blur(rb, sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
             yield y0, y1, out[y0 - a:y1 - a]
 
     cmax = torch.zeros(C, dtype=torch.float32, device=dev)

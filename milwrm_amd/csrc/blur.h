@@ -54,6 +54,13 @@ struct BlurEpi {
   const float* b;
   const float* centers;    //   k x C, scaled space
   int k;
+  // row window (fused epilogues): the input array holds slide rows [row_off,
+  // row_off + H); only array rows [r0, r1) are output (the rows around them
+  // are read as the vertical halo), and the side data (slots, mask) and the
+  // per-pixel outputs (lab, conf) are indexed by SLIDE pixel (row + row_off) *
+  // W + x -- a slide streamed band by band gives the whole-slide results
+  int64_t row_off;
+  int r0, r1;
 };
 
 template <typename T>
@@ -343,12 +350,8 @@ int launch_blur_valu(const T* in, int H, int W, int C, const float* inv_mean, fl
   if (C % 2 != 0 || C > 64 || r < 0 || r > kBlurMaxR) return MW_EUNSUPPORTED;
   switch (r) {
 #define MW_R(N) case N: return launch_blur_r<T, N>(in, H, W, C, inv_mean, p, taps, out, st);
-#ifdef MW_BLUR_DEV
-    MW_R(8)
-#else
     MW_R(0) MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8) MW_R(9) MW_R(10)
     MW_R(11) MW_R(12)
-#endif
 #undef MW_R
     default: return MW_EUNSUPPORTED;
   }

@@ -157,11 +157,7 @@ struct BlurMfmaCfg {
   // raw ring depth: as deep as two workgroups per CU allow (160 KB of LDS),
   // up to DMAX rows (the DMA of row s+2 is waited for at step s: LA-2 steps
   // of lead); one workgroup per CU only when two do not fit a 4-row ring
-#ifdef MW_BLUR_D
-  static constexpr int DMAX = MW_BLUR_D;
-#else
   static constexpr int DMAX = 8;
-#endif
   static constexpr int D2 = ((80 * 1024 - (int)FIXED) / SLOT);
   static constexpr int D1 = ((160 * 1024 - (int)FIXED) / SLOT);
   static constexpr int D = D2 >= 4 ? (D2 < DMAX ? D2 : DMAX) : (D1 >= 4 ? (D1 < DMAX ? D1 : DMAX) : 4);
@@ -186,11 +182,7 @@ __host__ __device__ __forceinline__ int blur_h16_unit(int x, int ct) {
 // log-normalised values are scaled by 2^8 before the split (the lo half stays
 // clear of f16 subnormals), the horizontal taps by 2^16; the vertical taps
 // take the 2^-24 back (exact: powers of two)
-#ifdef MW_BLUR_F32H
-constexpr bool kBlurH16 = false;  // A/B builds: horizontal pass on the f32 matrix cores
-#else
 constexpr bool kBlurH16 = true;   // log-normalised input: horizontal pass on f16 hi/lo products
-#endif
 constexpr float kH16XS = 256.f, kH16TS = 65536.f, kH16VS = 1.f / 16777216.f;
 
 // Band grid: nbx column bands x nby row bands of bh rows, one workgroup each,
@@ -203,6 +195,7 @@ constexpr float kH16XS = 256.f, kH16TS = 65536.f, kH16VS = 1.f / 16777216.f;
 // both for tuning.
 struct BlurGrid {
   int bh, nbx, ntiles, xcd;
+  int r0, r1;  // output rows [r0, r1) of the input array (the whole array but for streamed bands)
   __device__ __forceinline__ void tile(int b, int G, int& bx, int& by) const {
     const int x = b & 7, j = b >> 3, q = G >> 3, rem = G & 7;
     const int t = xcd ? x * q + (x < rem ? x : rem) + j : b;
@@ -211,14 +204,16 @@ struct BlurGrid {
   }
 };
 
-static inline BlurGrid blur_grid(int H, int nbx) {
+static inline BlurGrid blur_grid(int r0, int r1, int nbx) {
   BlurGrid g;
   g.nbx = nbx;
   g.bh = kBlurMfmaBH;
   g.xcd = 0;
+  g.r0 = r0;
+  g.r1 = r1;
   if (const char* e = getenv("MW_BLUR_BH")) g.bh = atoi(e) >= 16 ? atoi(e) : kBlurMfmaBH;
   if (const char* e = getenv("MW_BLUR_XCD")) g.xcd = atoi(e);
-  g.ntiles = nbx * ((H + g.bh - 1) / g.bh);
+  g.ntiles = nbx * ((r1 - r0 + g.bh - 1) / g.bh);
   return g;
 }
 
@@ -260,8 +255,8 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
   int bx, by;
   bg.tile(blockIdx.x, gridDim.x, bx, by);
   const int x0 = bx * BW;
-  const int y0 = by * bg.bh;
-  const int y1 = min(H, y0 + bg.bh);
+  const int y0 = bg.r0 + by * bg.bh;
+  const int y1 = min(bg.r1, y0 + bg.bh);
   const int nrows = (y1 - y0) + 2 * R;
   const int bw = min(BW, W - x0);
   // clamped input column range [xa, xb) and its position in the halo'd row
@@ -393,7 +388,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
           // from the 16-byte aligned address at or below its first pixel
           int yq = y0 + q - 2 - 2 * R;
           yq = yq < y0 ? y0 : (yq >= y1 ? y1 - 1 : yq);
-          const int64_t rp = (int64_t)yq * W + x0;
+          const int64_t rp = (int64_t)(yq + ep.row_off) * W + x0;  // slide pixel
           const char* asrc = EPI == kEpiSample
                                  ? reinterpret_cast<const char*>(ep.slots) + ((rp * 8) & ~(int64_t)15)
                                  : reinterpret_cast<const char*>(ep.mask) + (rp & ~(int64_t)15);
@@ -422,21 +417,15 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
         bf2 x = Chunk16<T>::pair(v, i);
         if constexpr (H16) {
           // x * 2^8 = hi + lo, both f16 (hi round-to-nearest, the residual exact in fp32)
-#ifdef MW_ABL_NOCONV
-          const h2m h = __builtin_convertvector(x, h2m), l = h;  // ablation: no log, no split
-#else
           x = log2norm2(x, p_inv[c * CP + i], pseudo) * bf2{kH16XS, kH16XS};
           const h2m h = __builtin_convertvector(x, h2m);
           const h2m l = __builtin_convertvector(x - __builtin_convertvector(h, bf2), h2m);
-#endif
           char* img = reinterpret_cast<char*>(dst) + p_dst[c * CP + i];
           *reinterpret_cast<h2m*>(img) = h;
           *reinterpret_cast<h2m*>(img + 2 * IMGH) = l;
           continue;
         }
-#ifndef MW_X_NOLOG
         if (LOGN) x = log2norm2(x, p_inv[c * CP + i], pseudo);  // log10(2): in the taps
-#endif
         const int d = p_dst[c * CP + i];
         *reinterpret_cast<bf2*>(d >= 0 ? dst + d : s_dummy) = x;  // pad pairs: the sink
       }
@@ -472,7 +461,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
   auto store_out = [&](int stg_buf, int yo, bool valid) {
     const f4m v = *reinterpret_cast<const f4m*>(s_stg + stg_buf * STG + 4 * t);
     const __amdgpu_buffer_rsrc_t ro =
-        blur_rsrc(out + ((int64_t)(valid ? yo : 0) * W + x0) * C, valid ? out_bytes : 0u);
+        blur_rsrc(out + ((int64_t)(valid ? yo - bg.r0 : 0) * W + x0) * C, valid ? out_bytes : 0u);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4m, v), ro, t * 16, 0, 0);
   };
 
@@ -480,7 +469,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
   auto epilogue = [&](int s) {
     asm volatile("" : "+s"(s));  // per-step values stay per step (no hoisting across the unroll)
     const int yo = y0 + s - 2 - 2 * R;
-    const int64_t rowpix = (int64_t)yo * W + x0;
+    const int64_t rowpix = (int64_t)(yo + ep.row_off) * W + x0;  // slide pixel (side data, outputs)
     const char* auxp = s_raw + (s % D) * SLOT + K::AUXOFF;
     const float* srow = s_stg + (s & 1) * STG + ecol * C;
     if constexpr (EPI == kEpiSample) {
@@ -538,7 +527,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
     asm volatile("" : "+s"(s));
     if (wv != (s % K::NW) || lane >= bw) return;
     const int yo = y0 + (s - 1) - 2 - 2 * R;
-    const int64_t rowpix = (int64_t)yo * W + x0;
+    const int64_t rowpix = (int64_t)(yo + ep.row_off) * W + x0;
     const float* dd = s_dist + ((s - 1) & 1) * kEpiKMax * BW + lane;
     int lab = 0;
     float m1 = dd[0], m2 = __builtin_inff();
@@ -595,11 +584,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
     if (!guard || (s >= 1 && s - 1 >= 2 * R && s - 1 < nrows)) {
       // vertical pass of row s-1 over ring rows s-1-2R .. s-1 (slots j .. j+2R)
       bf2 v0 = bf2{0.f, 0.f}, v1 = bf2{0.f, 0.f}, u0 = bf2{0.f, 0.f}, u1 = bf2{0.f, 0.f};
-#ifdef MW_ABL_NOVERT
-      constexpr int NRV = 1;  // ablation: one vertical tap
-#else
       constexpr int NRV = NR;
-#endif
 #pragma unroll
       for (int i = 0; i < NRV; ++i) {
         const f4m& rg = ring[(j + i) % NR];
@@ -626,9 +611,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
       }
     }
     if constexpr (EPI == kEpiStore) {
-#ifndef MW_ABL_NOSTORE
       store_out(s & 1, y0 + s - 2 - 2 * R, !guard || s >= 2 + 2 * R);
-#endif
     } else if (!guard || s >= 2 + 2 * R) {
       // kept apart from the other stages: interleaved, the epilogue's
       // temporaries would lift the kernel past 128 VGPRs (one workgroup per CU)
@@ -640,11 +623,6 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
     }
     dma_row(s + LA);
     if (!guard || s < nrows) {
-#ifdef MW_ABL_NOMFMA
-      if constexpr (H16) {  // ablation: no matrix-core work
-        ring[j] = __builtin_bit_cast(f4m, __builtin_shufflevector(b_hi, b_lo, 0, 1, 2, 3, 8, 9, 10, 11));
-      } else
-#endif
       if constexpr (H16) {
         // (hi + lo)(hi + lo) less lo*lo: three f16 products accumulated in fp32
         f4m d = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_hi, b_hi, f4m{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -700,7 +678,9 @@ static int launch_blur_mfma_one(const T* in, int H, int W, int C, const float* i
   const size_t lds = K::lds_bytes();
   if (lds > 160 * 1024 || K::D < 4) return MW_EUNSUPPORTED;
   const int nbx = (W + K::BW - 1) / K::BW;
-  const BlurGrid bg = blur_grid(H, nbx);
+  // the fused epilogues output the row window [ep.r0, ep.r1); img.blurring the whole array
+  const BlurGrid bg = EPI == kEpiStore ? blur_grid(0, H, nbx) : blur_grid(ep.r0, ep.r1, nbx);
+  if (bg.ntiles == 0) return MW_OK;
   BlurTaps tv = taps;  // H16: the vertical taps carry the 2^-24 descale (exact)
   if (LOGN && kBlurH16)
     for (int i = 0; i <= 2 * R; ++i) tv.w[i] = taps.w[i] * kH16VS;
@@ -726,18 +706,8 @@ static int launch_blur_mfma_r(const T* in, int H, int W, int C, const float* inv
   // at C <= 32).  128-column bands (one 16-wave workgroup per CU, 12.5 % halo
   // instead of 25 %) are 3 % faster in a blur-only loop (3.91-3.93 vs
   // 4.04-4.06 ms) but 1.5-2.5 % slower inside the bench step (4.02-4.07 vs
-  // 3.96-3.98 ms, same box, tools/dev/r3_bt_sweep.sh); development builds
-  // (-DMW_BLUR_BT8) keep them behind MW_BLUR_BT=8.
+  // 3.96-3.98 ms, same box, tools/dev/r3_bt_sweep.sh): not taken.
   const BlurEpi ep{};
-#ifdef MW_BLUR_BT8
-  static const int bt = [] {
-    const char* e = getenv("MW_BLUR_BT");
-    return (e && atoi(e) == 8) ? 8 : 4;
-  }();
-  if (bt == 8 && C <= 32)
-    return C <= 16 ? launch_blur_mfma_rc<T, R, 1, 8, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st)
-                   : launch_blur_mfma_rc<T, R, 2, 8, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
-#endif
   if (C <= 16) return launch_blur_mfma_rc<T, R, 1, 4, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
   if (C <= 32) return launch_blur_mfma_rc<T, R, 2, 4, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
   if (C <= 48) return launch_blur_mfma_rc<T, R, 3, 4, kEpiStore>(in, H, W, C, inv_mean, p, taps, out, ep, st);
@@ -785,11 +755,7 @@ int launch_blur_epi(const T* in, int H, int W, int C, const float* inv_mean, flo
   if (epi != kEpiSample && epi != kEpiAssign) return MW_EUNSUPPORTED;
   switch (r) {
 #define MW_R(N) case N: return launch_blur_epi_r<T, N>(in, H, W, C, inv_mean, p, taps, ep, epi, st);
-#ifdef MW_BLUR_DEV  // development builds: radius 8 only (sigma 2)
-    MW_R(8)
-#else
     MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8)
-#endif
 #undef MW_R
     default: return MW_EUNSUPPORTED;
   }
@@ -805,11 +771,7 @@ int launch_blur_mfma(const T* in, int H, int W, int C, const float* inv_mean, fl
     if (e[0] == 'v') return MW_EUNSUPPORTED;  // force the VALU kernel (A/B tests)
   switch (r) {
 #define MW_R(N) case N: return launch_blur_mfma_r<T, N>(in, H, W, C, inv_mean, p, taps, out, st);
-#ifdef MW_BLUR_DEV
-    MW_R(8)
-#else
     MW_R(1) MW_R(2) MW_R(3) MW_R(4) MW_R(5) MW_R(6) MW_R(7) MW_R(8)
-#endif
 #undef MW_R
     default: return MW_EUNSUPPORTED;
   }

@@ -750,36 +750,54 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 }
 __device__ __forceinline__ float u01(uint64_t h) { return ((h >> 40) + 0.5f) * (1.0f / 16777216.0f); }
 
-__global__ void synth_kernel(int H, int W, int C, const float* __restrict__ syx, int ns,
-                             const float* __restrict__ prof, int nd, int shape_k, int bg_rows,
-                             uint64_t seed, uint16_t* __restrict__ img, uint8_t* __restrict__ mask) {
-  const int64_t n = (int64_t)H * W;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += stride) {
-    const int y = (int)(p / W), x = (int)(p % W);
-    float best = 3.4e38f;
-    int dom = 0;
-    for (int s = 0; s < ns; ++s) {
-      const float dy = y - syx[2 * s], dx = x - syx[2 * s + 1];
-      const float d = dy * dy + dx * dx;
-      if (d < best) { best = d; dom = s % nd; }
-    }
-    const bool bg = y < bg_rows;
-    mask[p] = bg ? 0 : 1;
-    for (int c = 0; c < C; ++c) {
-      // Gamma(shape_k, 1/shape_k) as a mean of shape_k unit exponentials
-      float g = 0.f;
-      for (int k = 0; k < shape_k; ++k) {
-        const uint64_t h = splitmix64(seed ^ (((uint64_t)p * C + c) * 8 + k) * 0xD1B54A32D192ED03ull);
-        g += -__logf(u01(h));
+// Rows [y_beg, y_end) of the slide: every value is a function of its slide
+// pixel index alone (counter-based hash), so a band generated on its own is
+// bit for bit the same rows of the whole slide (streamed synthetic slides,
+// milwrm_amd.stream.SynthSource).  A block makes 256 consecutive pixels: the
+// values go through LDS and leave as one contiguous HWC run.
+constexpr int kSynthPx = 256;
+__global__ void __launch_bounds__(kSynthPx) synth_kernel(int W, int C, int y_beg, int y_end,
+                                                         const float* __restrict__ syx, int ns,
+                                                         const float* __restrict__ prof, int nd, int shape_k,
+                                                         int bg_rows, uint64_t seed, uint16_t* __restrict__ img,
+                                                         uint8_t* __restrict__ mask) {
+  extern __shared__ uint16_t s_px[];  // kSynthPx x C
+  const int64_t n = (int64_t)(y_end - y_beg) * W;
+  const int64_t p_base = (int64_t)y_beg * W;
+  for (int64_t base = (int64_t)blockIdx.x * kSynthPx; base < n; base += (int64_t)gridDim.x * kSynthPx) {
+    const int64_t pl = base + threadIdx.x;
+    if (pl < n) {
+      const int64_t p = p_base + pl;  // slide pixel
+      const int y = (int)(p / W), x = (int)(p % W);
+      float best = 3.4e38f;
+      int dom = 0;
+      for (int s = 0; s < ns; ++s) {
+        const float dy = y - syx[2 * s], dx = x - syx[2 * s + 1];
+        const float d = dy * dy + dx * dx;
+        if (d < best) { best = d; dom = s % nd; }
       }
-      g /= (float)shape_k;
-      float v = prof[dom * C + c] * g;
-      if (bg) v *= 0.05f;
-      v = rintf(v);
-      v = v < 0.f ? 0.f : (v > 65535.f ? 65535.f : v);
-      img[p * C + c] = (uint16_t)v;
+      const bool bg = y < bg_rows;
+      if (mask) mask[pl] = bg ? 0 : 1;
+      for (int c = 0; c < C; ++c) {
+        // Gamma(shape_k, 1/shape_k) as a mean of shape_k unit exponentials
+        float g = 0.f;
+        for (int k = 0; k < shape_k; ++k) {
+          const uint64_t h = splitmix64(seed ^ (((uint64_t)p * C + c) * 8 + k) * 0xD1B54A32D192ED03ull);
+          g += -__logf(u01(h));
+        }
+        g /= (float)shape_k;
+        float v = prof[dom * C + c] * g;
+        if (bg) v *= 0.05f;
+        v = rintf(v);
+        v = v < 0.f ? 0.f : (v > 65535.f ? 65535.f : v);
+        s_px[threadIdx.x * C + c] = (uint16_t)v;
+      }
     }
+    __syncthreads();
+    const int nel = (int)(n - base < kSynthPx ? n - base : (int64_t)kSynthPx) * C;
+    uint16_t* dst = img + base * C;
+    for (int e = threadIdx.x; e < nel; e += kSynthPx) dst[e] = s_px[e];
+    __syncthreads();
   }
 }
 
@@ -944,16 +962,8 @@ int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stre
   MW_CHECK_ARG(d_X && d_ws, "mw_col_stats_rows: null pointer");
   MW_CHECK_ARG(S > 0 && F > 0 && F <= 64, "mw_col_stats_rows: bad shape S=%lld F=%d", (long long)S, F);
   hipStream_t st = as_stream(stream);
-#ifdef MW_COL_STATS_LDS  // A/B: the LDS-tile form (gather_kernel without the gather)
-  size_t lds = (size_t)kTile * F * sizeof(float);
-  if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
-  hipLaunchKernelGGL(gather_kernel<false>, dim3(stream_blocks(S)), dim3(256), lds, st, nullptr, F,
-                     nullptr, F, nullptr, nullptr, S, rows_per_block(S), const_cast<float*>(d_X),
-                     reinterpret_cast<double*>(d_ws));
-#else
   hipLaunchKernelGGL(col_stats_rows_kernel, dim3(stream_blocks(S)), dim3(256), 0, st, d_X, F, S,
                      rows_per_block(S), reinterpret_cast<double*>(d_ws));
-#endif
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
@@ -992,7 +1002,43 @@ __global__ void __launch_bounds__(256) sample_overflow_kernel(const int32_t* __r
   }
 }
 
+// The sample epilogue as a pass of its own over a materialised fp32 band of
+// n pixels (slide pixels pix_off ..): X[j] = band[p - pix_off, feat] for both
+// table slots j of every sampled pixel p.  The streamed subsample of a slide
+// whose shape the fused kernel does not take (odd C, C > 64, radius > 8).
+__global__ void __launch_bounds__(256) slot_gather_kernel(const float* __restrict__ band, int C, int64_t n,
+                                                          int64_t pix_off, const int32_t* __restrict__ slots,
+                                                          int64_t S, const int32_t* __restrict__ feat, int F,
+                                                          float* __restrict__ X) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int2 sl = reinterpret_cast<const int2*>(slots)[pix_off + i];
+    if ((uint64_t)(uint32_t)sl.x >= (uint64_t)S) continue;
+    const bool two = (uint64_t)(uint32_t)sl.y < (uint64_t)S;
+    const float* src = band + i * C;
+    float* d0 = X + (int64_t)sl.x * F;
+    float* d1 = X + (int64_t)(two ? sl.y : sl.x) * F;
+    for (int f = 0; f < F; ++f) {
+      const float v = src[feat[f]];
+      d0[f] = v;
+      d1[f] = v;
+    }
+  }
+}
+
 size_t mw_sample_slot_elems(int64_t n_pix) { return 2 * ((size_t)n_pix + 128); }
+
+int mw_slot_gather(const float* d_band, int C, int64_t n_pix, int64_t pix_off, const int32_t* d_slots,
+                   int64_t S, const int32_t* d_feat, int F, float* d_X, void* stream) {
+  MW_CHECK_ARG(d_band && d_slots && d_feat && d_X, "mw_slot_gather: null pointer");
+  MW_CHECK_ARG(C > 0 && F > 0 && n_pix >= 0 && pix_off >= 0 && S > 0 && S < 0x7fffffffll,
+               "mw_slot_gather: bad args");
+  if (n_pix == 0) return MW_OK;
+  const int grid = (int)std::min<int64_t>((n_pix + 255) / 256, 16384);
+  hipLaunchKernelGGL(slot_gather_kernel, dim3(grid), dim3(256), 0, as_stream(stream), d_band, C, n_pix, pix_off,
+                     d_slots, S, d_feat, F, d_X);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
 
 int mw_sample_map(const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S, int64_t n_pix,
                   int32_t* d_slots, int32_t* d_ovf, void* stream) {
@@ -1049,29 +1095,44 @@ static int blur_epi_dispatch(const void* d_img, int dtype, int H, int W, int C, 
   return rc;
 }
 
-int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
-                   float pseudoval, const float* h_w, int radius, const int32_t* d_slots, int64_t S,
-                   const int32_t* d_feat, int F, float* d_X, void* stream) {
+int mw_blur_sample_rows(const void* d_img, int dtype, int H, int W, int C, int64_t row_off, int r0, int r1,
+                        const float* d_inv_mean, float pseudoval, const float* h_w, int radius,
+                        const int32_t* d_slots, int64_t S, const int32_t* d_feat, int F, float* d_X,
+                        void* stream) {
   MW_CHECK_ARG(d_img && d_inv_mean && h_w && d_slots && d_feat && d_X, "mw_blur_sample: null pointer");
   MW_CHECK_ARG(H > 0 && W > 0 && C > 0 && F > 0 && S > 0 && S < 0x7fffffffll,
                "mw_blur_sample: bad shape");
+  MW_CHECK_ARG(0 <= r0 && r0 <= r1 && r1 <= H && row_off >= 0, "mw_blur_sample: bad row window [%d, %d) of %d rows",
+               r0, r1, H);
   BlurEpi ep{};
   ep.slots = d_slots;
   ep.S = S;
   ep.X = d_X;
   ep.F = F;
   ep.feat = d_feat;
+  ep.row_off = row_off;
+  ep.r0 = r0;
+  ep.r1 = r1;
   return blur_epi_dispatch(d_img, dtype, H, W, C, d_inv_mean, pseudoval, h_w, radius, ep, kEpiSample,
                            stream, "mw_blur_sample");
 }
 
-int mw_blur_assign_conf(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
-                        float pseudoval, const float* h_w, int radius, const float* d_a,
-                        const float* d_b, const float* d_centers, int k, const uint8_t* d_mask,
-                        int8_t* d_label, float* d_conf, void* stream) {
+int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
+                   float pseudoval, const float* h_w, int radius, const int32_t* d_slots, int64_t S,
+                   const int32_t* d_feat, int F, float* d_X, void* stream) {
+  return mw_blur_sample_rows(d_img, dtype, H, W, C, 0, 0, H, d_inv_mean, pseudoval, h_w, radius, d_slots, S,
+                             d_feat, F, d_X, stream);
+}
+
+int mw_blur_assign_rows(const void* d_img, int dtype, int H, int W, int C, int64_t row_off, int r0, int r1,
+                        const float* d_inv_mean, float pseudoval, const float* h_w, int radius,
+                        const float* d_a, const float* d_b, const float* d_centers, int k,
+                        const uint8_t* d_mask, int8_t* d_label, float* d_conf, void* stream) {
   MW_CHECK_ARG(d_img && d_inv_mean && h_w && d_a && d_b && d_centers && d_mask && d_label && d_conf,
                "mw_blur_assign_conf: null pointer");
   MW_CHECK_ARG(H > 0 && W > 0 && C > 0 && k >= 1, "mw_blur_assign_conf: bad shape");
+  MW_CHECK_ARG(0 <= r0 && r0 <= r1 && r1 <= H && row_off >= 0,
+               "mw_blur_assign_conf: bad row window [%d, %d) of %d rows", r0, r1, H);
   BlurEpi ep{};
   ep.mask = d_mask;
   ep.lab = d_label;
@@ -1080,8 +1141,19 @@ int mw_blur_assign_conf(const void* d_img, int dtype, int H, int W, int C, const
   ep.b = d_b;
   ep.centers = d_centers;
   ep.k = k;
+  ep.row_off = row_off;
+  ep.r0 = r0;
+  ep.r1 = r1;
   return blur_epi_dispatch(d_img, dtype, H, W, C, d_inv_mean, pseudoval, h_w, radius, ep, kEpiAssign,
                            stream, "mw_blur_assign_conf");
+}
+
+int mw_blur_assign_conf(const void* d_img, int dtype, int H, int W, int C, const float* d_inv_mean,
+                        float pseudoval, const float* h_w, int radius, const float* d_a,
+                        const float* d_b, const float* d_centers, int k, const uint8_t* d_mask,
+                        int8_t* d_label, float* d_conf, void* stream) {
+  return mw_blur_assign_rows(d_img, dtype, H, W, C, 0, 0, H, d_inv_mean, pseudoval, h_w, radius, d_a, d_b,
+                             d_centers, k, d_mask, d_label, d_conf, stream);
 }
 
 int mw_col_stats_finalize(const void* d_ws, int64_t S, int F, double* d_stats, int accumulate,
@@ -1101,18 +1173,29 @@ int mw_col_stats_absmax(const void* d_ws, int64_t S, int F, float* d_out, int ac
   return MW_OK;
 }
 
+int mw_synth_rows(int H, int W, int C, int y0, int y1, const float* d_seed_yx, int n_seeds,
+                  const float* d_profiles, int n_domains, int shape_k, int bg_rows, uint64_t seed,
+                  uint16_t* d_img, uint8_t* d_mask, void* stream) {
+  MW_CHECK_ARG(d_seed_yx && d_profiles && d_img, "mw_synth_rows: null pointer");
+  MW_CHECK_ARG(H > 0 && W > 0 && C > 0 && C <= 128 && n_seeds > 0 && n_domains > 0 && shape_k > 0,
+               "mw_synth_rows: bad args (C <= 128)");
+  MW_CHECK_ARG(0 <= y0 && y0 <= y1 && y1 <= H, "mw_synth_rows: rows [%d, %d) of %d", y0, y1, H);
+  const int64_t n = (int64_t)(y1 - y0) * W;
+  if (n == 0) return MW_OK;
+  const int grid = (int)std::min<int64_t>((n + kSynthPx - 1) / kSynthPx, 65536);
+  hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(kSynthPx), (size_t)kSynthPx * C * sizeof(uint16_t),
+                     as_stream(stream), W, C, y0, y1, d_seed_yx, n_seeds, d_profiles, n_domains, shape_k,
+                     bg_rows, seed, d_img, d_mask);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
 int mw_synth_slide(int H, int W, int C, const float* d_seed_yx, int n_seeds, const float* d_profiles,
                    int n_domains, int shape_k, int bg_rows, uint64_t seed, uint16_t* d_img,
                    uint8_t* d_mask, void* stream) {
-  MW_CHECK_ARG(d_seed_yx && d_profiles && d_img && d_mask, "mw_synth_slide: null pointer");
-  MW_CHECK_ARG(H > 0 && W > 0 && C > 0 && n_seeds > 0 && n_domains > 0 && shape_k > 0,
-               "mw_synth_slide: bad args");
-  const int64_t n = (int64_t)H * W;
-  const int grid = (int)std::min<int64_t>((n + 255) / 256, 65536);
-  hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(256), 0, as_stream(stream), H, W, C, d_seed_yx,
-                     n_seeds, d_profiles, n_domains, shape_k, bg_rows, seed, d_img, d_mask);
-  MW_LAUNCH_CHECK();
-  return MW_OK;
+  MW_CHECK_ARG(d_mask, "mw_synth_slide: null pointer");
+  return mw_synth_rows(H, W, C, 0, H, d_seed_yx, n_seeds, d_profiles, n_domains, shape_k, bg_rows, seed,
+                       d_img, d_mask, stream);
 }
 
 }  // extern "C"

@@ -328,7 +328,9 @@ def col_stats_rows(X: torch.Tensor, stats: torch.Tensor, accumulate: bool, absma
         N.call("mw_col_stats_absmax", P(ws), S, F, P(absmax), 1, stream())
 
 
-FUSED_USED = {"sample": 0, "assign": 0, "assign_banded": 0}  # deferred-blur paths taken (tests read it)
+# deferred-blur paths taken (tests read it); *_streamed: over a slide read band by band (stream.py)
+FUSED_USED = {"sample": 0, "assign": 0, "assign_banded": 0, "sample_streamed": 0, "assign_streamed": 0,
+              "nz_streamed": 0}
 
 
 def defer_blur(H: int, W: int, C: int) -> bool:
@@ -361,46 +363,26 @@ def blur_gather_fused(img: torch.Tensor, sigma: float, inv_mean, pseudoval: floa
                       feat: torch.Tensor, idx: torch.Tensor, r2p: torch.Tensor, X_out: torch.Tensor,
                       truncate: float = 4.0) -> bool:
     """X_out[j] = blur(lognorm(img))[r2p[idx[j]], feat] without storing the
-    blurred slide: sample map (per pixel its first two sample slots, later
-    draws on an overflow list) → blur with the sample epilogue, which writes
-    both table slots → overflow copies.  False (nothing done) when the fused
-    kernel does not take this shape; the caller then materialises the blur
-    and gathers."""
-    H, W, C = img.shape
-    S, F = X_out.shape
-    if S == 0 or inv_mean is None:
-        return False
-    w = gaussian_taps(sigma, truncate)
-    r = (len(w) - 1) // 2
-    n = H * W
-    slots = WS.get("sample_slots", 4 * N.query("mw_sample_slot_elems", n))
-    ovf = WS.get("sample_ovf", 4 * (S + 1))
-    st = stream()
-    with profiling.timed("sample_map", S * 16):
-        N.call("mw_sample_map", P(idx), P(r2p), S, n, P(slots), P(ovf), st)
-    with profiling.timed("blur_sample", n * C * img.element_size() + S * F * 4):
-        ok = N.try_call("mw_blur_sample", P(img), dtype_code(img), H, W, C, P(inv_mean),
-                        float(pseudoval), w.ctypes.data, r, P(slots), S, P(feat), F, P(X_out), st)
-    if not ok:
-        return False
-    with profiling.timed("sample_overflow", S * 0):
-        N.call("mw_sample_overflow", P(idx), P(r2p), P(slots), P(ovf), S, F, P(X_out), st)
-    FUSED_USED["sample"] += 1
-    return True
+    blurred slide (stream.blur_gather over the resident slide as one band):
+    sample map (per pixel its first two sample slots, later draws on an
+    overflow list) → blur with the sample epilogue, which writes both table
+    slots → overflow copies.  False (nothing done) when nothing is sampled."""
+    from .stream import blur_gather
+
+    return blur_gather(img, sigma, inv_mean, pseudoval, feat, idx, r2p, X_out, truncate)
 
 
-def synth_slide(H, W, C, seed, mode="hard", n_seeds=32, n_domains=8, bg_frac=0.15):
+def synth_slide(H, W, C, seed, mode="hard"):
     """Benchmark input generated on device (SURVEY §8d shape): uint16 HWC
     (int16 storage) + uint8 mask."""
-    rng = np.random.default_rng(seed)
-    sp_, shape = (0.15, 1) if mode == "hard" else (0.8, 4)
-    syx = np.stack([rng.uniform(0, H, n_seeds), rng.uniform(0, W, n_seeds)], 1).astype(np.float32)
-    prof = rng.lognormal(4.0, sp_, size=(n_domains, C)).astype(np.float32)
+    from .stream import _synth_params
+
+    syx, prof, shape, bg_rows, n_seeds, n_domains = _synth_params(H, W, C, seed, mode)
     dev = device()
     d_syx = torch.from_numpy(syx.ravel()).to(dev)
     d_prof = torch.from_numpy(prof.ravel()).to(dev)
     img = torch.empty((H, W, C), dtype=torch.int16, device=dev)
     mask = torch.empty((H, W), dtype=torch.uint8, device=dev)
     N.call("mw_synth_slide", H, W, C, P(d_syx), n_seeds, P(d_prof), n_domains, shape,
-           int(round(bg_frac * H)), int(seed) & 0xFFFFFFFFFFFFFFFF, P(img), P(mask), stream())
+           bg_rows, int(seed) & 0xFFFFFFFFFFFFFFFF, P(img), P(mask), stream())
     return img, mask

@@ -280,10 +280,10 @@ def _check_fit_memory(rows: DeviceRows, ks) -> None:
     any allocation so a too-large sweep raises with the remedy instead of
     failing inside torch (find_optimal_k runs 19 fits together)."""
     S, F = rows.S, rows.F
+    from .stream import RESIDENCY
+
     need = sum(S * 9 + N.query("mw_lloyd_ws_bytes", S, k, F) for k in ks)
-    dev = rows.X.device
-    free, _ = torch.cuda.mem_get_info(dev)
-    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    free = RESIDENCY.release(need)  # resident copies of host-backed slides go first (stream.py)
     if need > free:
         raise MemoryError(
             f"{len(ks)} k-means fits over {S} rows need {need / 2**30:.1f} GiB of HBM for their "
@@ -724,6 +724,9 @@ class KMeans:
         inertia, n_iter = C.c_double(), C.c_int()
         idx = np.full(k, -1, dtype=np.int64)
         nb = N.query("mw_kmeans_fit_ws_bytes", S, F, k)
+        from .stream import RESIDENCY
+
+        RESIDENCY.release(nb + S + (64 << 20))  # workspace + labels; host-backed slide copies go first
         ws = D.WS.get("kfit", nb)
         with profiling.timed("kmeans_fit", 0):
             N.call("mw_kmeans_fit", D.P(rows.X), S, F, mu.ctypes.data, inv.ctypes.data,

@@ -156,3 +156,43 @@ def test_lloyd_workspace_holds_records_and_row_lists():
         ws = N.query("mw_lloyd_ws_bytes", S, k, F)
         rec = N.query("mw_lloyd_rec_len", k, F) * 8
         assert ws >= rec + 4 * S, (S, k, F, ws)
+
+
+def test_stream_band_plan_covers_rows():
+    """stream.bands over a resident source (views, no GPU needed): output rows
+    tile [r0, r1) once, each band's raw rows are its output rows plus the
+    halo clipped to the slide."""
+    import torch
+
+    from milwrm_amd import stream
+
+    H = 53
+    t = torch.arange(H * 3 * 2, dtype=torch.int16).reshape(H, 3, 2)
+    src = stream.DeviceSource(t)
+    for band, halo, r0, r1 in [(7, 3, 0, H), (53, 8, 0, H), (1, 0, 0, H), (10, 8, 5, 41), (100, 2, 0, H)]:
+        seen = []
+        for y0, y1, a, raw in stream.bands(src, band, halo, r0, r1):
+            assert a == max(0, y0 - halo)
+            assert raw.shape[0] == min(H, y1 + halo) - a
+            assert torch.equal(raw, t[a:a + raw.shape[0]])
+            seen.extend(range(y0, y1))
+        assert seen == list(range(r0, r1))
+
+
+def test_stream_parse_bytes_and_host_dtypes():
+    import torch
+
+    from milwrm_amd import stream
+
+    assert stream._parse_bytes("64G") == 64 << 30
+    assert stream._parse_bytes("1.5M") == int(1.5 * (1 << 20))
+    assert stream._parse_bytes("12345") == 12345
+    assert stream.device_dtype_of(np.zeros((2, 2, 2), np.uint8)) == torch.uint8
+    assert stream.device_dtype_of(np.zeros((2, 2, 2), np.uint16)) == torch.int16
+    assert stream.device_dtype_of(np.full((2, 2, 2), 70000, np.int32)) == torch.float32
+    assert stream.device_dtype_of(np.full((2, 2, 2), 700, np.int64)) == torch.int16
+    assert stream.device_dtype_of(np.zeros((2, 2, 2), np.float64)) == torch.float32
+    hs = stream.HostSource(np.arange(5 * 4 * 3, dtype=np.uint16).reshape(5, 4, 3) + 60000)
+    rows = hs._host_rows(1, 3)
+    assert rows.dtype == torch.int16 and tuple(rows.shape) == (2, 4, 3)
+    assert int(rows.view(torch.int16).to(torch.int32)[0, 0, 0]) & 0xFFFF == 60000 + 12

@@ -130,11 +130,97 @@ def _check_label_pass(raw, mask, lab, mean, smu, sinv, n=100_000, seed=0, step=5
     assert worst < RTOL, worst
 
 
+def _lloyd64(lab, smu, sinv, step=2_000_000):
+    """Test infrastructure: sklearn's ``_kmeans_single_lloyd`` (_kmeans.py:
+    624-752, as oracle.lloyd) in fp64 torch on the device, from the fit's own
+    k-means++ indices over the same fp32 rows (direct-difference distances,
+    lowest index wins ties, strict label convergence or the center-shift
+    tolerance, the extra E-step when not strict).  Returns (labels int64,
+    centers fp64, n_iter, strict, gap) with gap = the relative top-2 distance
+    gap of every row under the final centers."""
+    rows = lab._rows
+    S, F = rows.S, rows.F
+    km = lab.kmeans
+    k = km.cluster_centers_.shape[0]
+    dev = rows.X.device
+    idx = torch.from_numpy(np.asarray(km.init_indices_, dtype=np.int64)).to(dev)
+    centers = (rows.X.index_select(0, idx).double() - smu) * sinv
+    tol = float(np.mean(lab.scaler.var_ / lab.scaler.scale_ ** 2)) * km.tol
+    labels_old = torch.full((S,), -1, dtype=torch.int64, device=dev)
+
+    def estep(C, want_gap=False):
+        lab_ = torch.empty(S, dtype=torch.int64, device=dev)
+        gap = torch.empty(S, dtype=torch.float64, device=dev) if want_gap else None
+        sums = torch.zeros((k, F), dtype=torch.float64, device=dev)
+        for a, b in _chunks(S, step):
+            xs = (rows.X[a:b].double() - smu) * sinv
+            d = torch.stack([((xs - C[j]) ** 2).sum(1) for j in range(k)], 1)
+            lab_[a:b] = d.argmin(1)
+            if want_gap:
+                top = torch.topk(d, 2, dim=1, largest=False).values
+                gap[a:b] = (top[:, 1] - top[:, 0]) / top[:, 1]
+            sums.index_add_(0, lab_[a:b], xs)
+        cnt = torch.bincount(lab_, minlength=k).double()
+        return lab_, sums, cnt, gap
+
+    strict = False
+    for it in range(km.max_iter):
+        labels, sums, cnt, _ = estep(centers)
+        assert bool((cnt > 0).all()), "empty cluster: relocation is outside this check"
+        new = sums / cnt[:, None]
+        shift = float(((new - centers) ** 2).sum())
+        centers = new
+        if torch.equal(labels, labels_old):
+            strict = True
+            break
+        if shift <= tol:
+            break
+        labels_old = labels
+    labels, _, _, gap = estep(centers, want_gap=True)
+    return labels, centers, it + 1, strict, gap
+
+
+def _check_mstep(lab, smu, sinv):
+    """The fit against the fp64 Lloyd from the same k-means++ indices: the same
+    n_iter, labels equal outside near-ties, centers within 1e-4."""
+    km = lab.kmeans
+    labels, centers, n_iter, strict, gap = _lloyd64(lab, smu, sinv)
+    assert n_iter == km.n_iter_, (n_iter, km.n_iter_, strict)
+    diff = (labels != km._labels_dev.long()) & ~(gap < TAU)
+    assert int(diff.sum()) == 0, f"{int(diff.sum())} fit labels differ from the fp64 Lloyd outside near-ties"
+    c = centers.cpu().numpy()
+    scale = np.abs(c).max()
+    np.testing.assert_allclose(km.cluster_centers_, c, rtol=1e-4, atol=1e-4 * scale)
+
+
+def _check_centers_are_means(lab, smu, sinv, step=2_000_000):
+    """At the Lloyd fixed point the centers are the per-label means of the
+    scaled rows: within 1e-4 (strict convergence), else within the fit's
+    center-shift tolerance."""
+    rows = lab._rows
+    S, F = rows.S, rows.F
+    km = lab.kmeans
+    k = km.cluster_centers_.shape[0]
+    labels = km._labels_dev.long()
+    sums = torch.zeros((k, F), dtype=torch.float64, device=rows.X.device)
+    for a, b in _chunks(S, step):
+        sums.index_add_(0, labels[a:b], (rows.X[a:b].double() - smu) * sinv)
+    cnt = torch.bincount(labels, minlength=k).double()
+    means = (sums / cnt[:, None]).cpu().numpy()
+    c = km.cluster_centers_
+    if np.abs(c - means).max() <= 1e-4 * np.abs(means).max():
+        return
+    tol = float(np.mean(lab.scaler.var_ / lab.scaler.scale_ ** 2)) * km.tol
+    assert ((c - means) ** 2).sum() <= tol, (np.abs(c - means).max(), tol)
+
+
 @pytest.mark.timeout(900)
 def test_config2_full_size(gpu):
     """Config 2: one 10k x 10k x 30 hard slide, k = 8 (the bench workload)."""
     raw, mask, lab, mean = _run(10_000, 30, 8, 20251015)
     smu, sinv = _check_scaler_fit(lab, 8)
+    _check_mstep(lab, smu, sinv)
+    _check_centers_are_means(lab, smu, sinv)
     # k-means++ at the bench's size: the oracle on the full row set
     rows = lab._rows
     Xs = ((rows.X.double() - smu) * sinv).cpu().numpy()
@@ -157,4 +243,9 @@ def test_config5_slide_full_size(gpu):
     raw, mask, lab, mean = _run(40_000, 50, 8, 20251016)
     assert D.FUSED_USED["sample"] > used["sample"]  # the 320 GB fp32 slide was never stored
     smu, sinv = _check_scaler_fit(lab, 8)
+    _check_centers_are_means(lab, smu, sinv)
+    from milwrm_amd.rng import first_center_index, kpp_draws
+
+    u0, _ = kpp_draws(18, 8, 2 + int(np.log(8)))
+    assert int(lab.kmeans.init_indices_[0]) == first_center_index(lab._rows.S, u0)
     _check_label_pass(raw, mask, lab, mean, smu, sinv, step=2_000)

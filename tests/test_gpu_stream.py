@@ -1,0 +1,260 @@
+"""Slide residency and streaming (milwrm_amd.stream; SURVEY §7 step 8,
+BASELINE config 5: more slides per GPU than HBM holds).
+
+* An HBM budget cap (``MW_HBM_BUDGET``) forces every host-backed slide to be
+  streamed in row bands (non-zero statistics, blur + subsample epilogue over
+  output-row windows, banded blur + label pass, QC sums); the results must be
+  BITWISE those of the resident run: scaler, k-means++ indices, n_iter,
+  centers, inertia, every row label, every pixel's label and confidence, the
+  confidence frame, the QC estimators.  Shapes cover the matrix-core
+  epilogues (C = 8, 50) and the slot-gather fallback (odd C), odd band sizes.
+* A budget that holds one slide at a time: the LRU evicts, results unchanged.
+* The synthetic source's bands are bit for bit the whole generated slide.
+* Two 40k x 40k x 50 slides on one GPU (config 5's two slides per GPU of an
+  8-GPU node), streamed from the device generator: property checks as
+  tests/test_gpu_fullsize.py (scaler, first k-means++ index, fit labels and
+  inertia against fp64 recomputes, sampled pixels' labels / confidences
+  against an fp64 blur of regenerated raw rows).
+"""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from oracle import milwrm_oracle as O
+
+pytestmark = pytest.mark.gpu
+TAU = 1e-5
+
+
+def _slides(C, n=3, seed=900, dtype=np.uint16):
+    out = []
+    for i in range(n):
+        raw, mask = O.synth_slide(150 + 17 * i, 176 + 32 * i, C, seed=seed + i, mode="hard")
+        out.append((np.minimum(raw, 255).astype(dtype) if dtype != np.uint16 else raw, mask))
+    return out
+
+
+def _pipeline(slides, k=5, qc=True):
+    import milwrm_amd as M
+    from milwrm_amd.MILWRM import estimate_mse_mxif, estimate_percentage_variance_mxif
+
+    C = slides[0][0].shape[2]
+    imgs = [M.img(r.copy(), mask=m.copy()) for r, m in slides]
+    ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
+    df = pd.DataFrame({"Img": imgs, "batch_names": ["b1", "b1", "b2"][:len(imgs)],
+                       "mean estimators": list(ests), "pixels": list(pix)})
+    lab = M.mxif_labeler(df)
+    lab.prep_cluster_data(features=list(range(C)), sigma=2, fract=0.2)
+    lab.label_tissue_regions(k=k, plot_out=False, random_state=18)
+    lab.confidence_score_images()
+    out = dict(est=np.asarray(ests), pix=np.asarray(pix), mean=lab.scaler.mean_,
+               scale=lab.scaler.scale_, idx=lab.kmeans.init_indices_, n_iter=lab.kmeans.n_iter_,
+               centers=lab.kmeans.cluster_centers_, inertia=lab.kmeans.inertia_,
+               rows=lab.kmeans.labels_, conf_df=lab.confidence_score_df.values,
+               tid=[np.nan_to_num(t, nan=-1) for t in lab.tissue_IDs],
+               cid=[np.nan_to_num(c, nan=-1) for c in lab.confidence_IDs],
+               np_state=np.random.get_state()[1].copy())
+    if qc:
+        feats = list(range(C))
+        out["pv"] = [estimate_percentage_variance_mxif(im, False, lab.scaler, lab.kmeans.cluster_centers_,
+                                                       feats, t) for im, t in zip(imgs, lab.tissue_IDs)]
+        mse = estimate_mse_mxif(imgs, False, list(lab.tissue_IDs), lab.scaler, lab.kmeans.cluster_centers_,
+                                feats, k)
+        out["mse"] = np.array([mse[i] for i in range(k)])
+    out["resident"] = [im._dev is not None for im in imgs]
+    return out
+
+
+def _assert_same(a, b):
+    for key in ("est", "pix", "mean", "scale", "idx", "centers", "rows", "conf_df", "np_state"):
+        np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+    assert a["n_iter"] == b["n_iter"]
+    assert a["inertia"] == b["inertia"]
+    for x, y in zip(a["tid"], b["tid"]):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(a["cid"], b["cid"]):
+        np.testing.assert_array_equal(x, y)
+    if "pv" in a:
+        np.testing.assert_array_equal(a["pv"], b["pv"])
+        np.testing.assert_array_equal(a["mse"], b["mse"])
+
+
+@pytest.mark.parametrize("C,dtype,band", [(8, np.uint16, "37"), (50, np.uint16, "61"), (7, np.uint16, "29"),
+                                          (8, np.uint8, "200")])
+def test_streamed_equals_resident(gpu, monkeypatch, C, dtype, band):
+    from milwrm_amd import device as D
+
+    slides = _slides(C, dtype=dtype)
+    monkeypatch.delenv("MW_HBM_BUDGET", raising=False)
+    ref = _pipeline(slides)
+    assert all(ref["resident"])
+    monkeypatch.setenv("MW_HBM_BUDGET", "1")       # nothing may stay resident: every pass streams
+    monkeypatch.setenv("MW_STREAM_BAND_ROWS", band)
+    before = dict(D.FUSED_USED)
+    got = _pipeline(slides)
+    assert not any(got["resident"])
+    for key in ("nz_streamed", "sample_streamed", "assign_streamed"):
+        assert D.FUSED_USED[key] > before[key], key
+    _assert_same(got, ref)
+
+
+def test_fused_assign_streamed(gpu, monkeypatch):
+    """The fused blur + label epilogue over streamed bands (mw_blur_assign_rows)
+    gives the banded path's bits."""
+    from milwrm_amd import device as D
+
+    slides = _slides(8)
+    monkeypatch.setenv("MW_HBM_BUDGET", "1")
+    monkeypatch.setenv("MW_STREAM_BAND_ROWS", "45")
+    ref = _pipeline(slides, qc=False)
+    monkeypatch.setenv("MW_DEFERRED_ASSIGN", "fused")
+    before = dict(D.FUSED_USED)
+    got = _pipeline(slides, qc=False)
+    assert D.FUSED_USED["assign"] > before["assign"]
+    _assert_same(got, ref)
+
+
+def test_lru_eviction(gpu, monkeypatch):
+    """A budget that holds about one slide: uploads evict the least recently
+    used copy (host arrays stay), the fit releases what it needs; the results
+    do not change."""
+    from milwrm_amd.stream import RESIDENCY
+
+    slides = _slides(8)
+    ref = _pipeline(slides)
+    one = max(r.shape[0] * r.shape[1] * r.shape[2] * 4 for r, _ in slides)  # an fp32 blurred copy
+    monkeypatch.setenv("MW_HBM_BUDGET", str(int(one * 1.2)))
+    ev = RESIDENCY.evictions
+    got = _pipeline(slides)
+    assert RESIDENCY.evictions > ev
+    assert RESIDENCY.used() <= one * 1.2
+    _assert_same(got, ref)
+
+
+def test_synth_source_bands_bitwise(gpu):
+    from milwrm_amd import device as D
+    from milwrm_amd import stream
+
+    H, W, C = 301, 208, 50
+    raw, mask = D.synth_slide(H, W, C, seed=77)
+    src = stream.SynthSource(H, W, C, 77)
+    whole = src.materialize()
+    assert torch.equal(whole, raw)
+    assert torch.equal(src.mask_device(), mask)
+    got = torch.empty_like(raw)
+    for y0, y1, a, rb in stream.bands(src, 23, 8):
+        got[a:a + rb.shape[0]] = rb
+    assert torch.equal(got, raw)
+
+
+# ------------------------------------------------- two config-5 slides / GPU
+
+def _chunks(n, step):
+    for a in range(0, n, step):
+        yield a, min(n, a + step)
+
+
+def _blur64_rows(src, mean, ys, xs, sigma=2.0):
+    """fp64 log10(x/mean + 1) + the scipy Gaussian (mode='nearest') at pixels
+    (ys, xs), from raw rows the source regenerates."""
+    H, W, C = src.shape
+    w = torch.from_numpy(O.gaussian_kernel1d(sigma)).cuda()
+    r = (w.numel() - 1) // 2
+    y0, y1 = max(0, int(ys.min()) - r), min(H, int(ys.max()) + r + 1)
+    rows = torch.empty((y1 - y0, W, C), dtype=src.dtype, device="cuda")
+    src.read(y0, y1, rows)
+    off = torch.arange(-r, r + 1, device="cuda")
+    yy = (ys[:, None] + off[None]).clamp(0, H - 1) - y0
+    xx = (xs[:, None] + off[None]).clamp(0, W - 1)
+    p = rows[yy[:, :, None], xx[:, None, :]]
+    p = (p.to(torch.int32) & 0xFFFF).double()
+    inv = torch.from_numpy(1.0 / mean).cuda()
+    p = torch.log10(p * inv + 1.0)
+    v = (p * w[None, :, None, None]).sum(1)
+    return (v * w[None, :, None]).sum(1)
+
+
+@pytest.mark.timeout(1200)
+def test_two_config5_slides_streamed(gpu):
+    """Config 5's per-GPU share on an 8-GPU node: two 40k x 40k x 50 slides
+    (160 GB of uint16 each: they cannot both be resident), streamed band by
+    band from the device generator, k = 8."""
+    import milwrm_amd as M
+    from milwrm_amd import device as D
+    from milwrm_amd import stream
+    from milwrm_amd.rng import first_center_index, kpp_draws
+
+    D.WS.clear()
+    torch.cuda.empty_cache()
+    H = W = 40_000
+    C = 50
+    srcs = [stream.SynthSource(H, W, C, 20251016 + i) for i in range(2)]
+    imgs = [M.img.from_source(s) for s in srcs]
+    before = dict(D.FUSED_USED)
+    ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
+    df = pd.DataFrame({"Img": imgs, "batch_names": ["b", "b"], "mean estimators": list(ests),
+                       "pixels": list(pix)})
+    lab = M.mxif_labeler(df)
+    lab.prep_cluster_data(features=list(range(C)), sigma=2, fract=0.2)
+    lab.label_tissue_regions(k=8, plot_out=False, random_state=18)
+    lab.confidence_score_images()
+    assert all(im._dev is None for im in imgs)  # never resident
+    for key in ("nz_streamed", "sample_streamed", "assign_streamed"):
+        assert D.FUSED_USED[key] >= before[key] + 2, key
+    mean = (np.asarray(ests[0]) + np.asarray(ests[1])) / (pix[0] + pix[1])
+    # scaler against an fp64 recompute of the gathered rows
+    rows = lab._rows
+    S, F = rows.S, rows.F
+    assert S == sum(lab._batch_counts)
+    step = 2_000_000
+    s1 = torch.zeros(F, dtype=torch.float64, device="cuda")
+    for a, b in _chunks(S, step):
+        s1 += rows.X[a:b].double().sum(0)
+    mu = s1 / S
+    s2 = torch.zeros(F, dtype=torch.float64, device="cuda")
+    for a, b in _chunks(S, step):
+        s2 += ((rows.X[a:b].double() - mu) ** 2).sum(0)
+    np.testing.assert_allclose(lab.scaler.mean_, mu.cpu().numpy(), rtol=1e-11, atol=1e-13)
+    np.testing.assert_allclose(lab.scaler.var_, (s2 / S).cpu().numpy(), rtol=1e-9)
+    # first k-means++ center (sklearn's sequential cumsum of 1/n, rng.first_center_index)
+    u0, _ = kpp_draws(18, 8, 2 + int(np.log(8)))
+    assert int(lab.kmeans.init_indices_[0]) == first_center_index(S, u0)
+    # fit labels = fp64 argmin under the final centers (near-ties aside), inertia
+    km = lab.kmeans
+    smu = torch.from_numpy(lab.scaler.mean_).cuda()
+    sinv = torch.from_numpy(1.0 / lab.scaler.scale_).cuda()
+    Cn = torch.from_numpy(km.cluster_centers_).cuda()
+    labels = km._labels_dev.long()
+    inertia, bad = 0.0, 0
+    for a, b in _chunks(S, step):
+        xs = (rows.X[a:b].double() - smu) * sinv
+        inertia += float(((xs - Cn[labels[a:b]]) ** 2).sum())
+        d = ((xs[:, None, :] - Cn[None]) ** 2).sum(-1)
+        top = torch.topk(d, 2, dim=1, largest=False).values
+        gap = (top[:, 1] - top[:, 0]) / top[:, 1]
+        bad += int(((d.argmin(1) != labels[a:b]) & ~(gap < TAU)).sum())
+    assert abs(km.inertia_ - inertia) <= 1e-6 * inertia, (km.inertia_, inertia)
+    assert bad == 0
+    # label pass: sampled pixels in a few row windows (top edge, interior, bottom edge)
+    g = torch.Generator().manual_seed(5)
+    for s, (src, im) in enumerate(zip(srcs, imgs)):
+        L, Cf = lab._labels_dev[s], lab._conf_dev[s]
+        mask = src.mask_device()
+        nbad, worst = 0, 0.0
+        for wy in (0, 5_003, 19_990, 39_800):
+            ys = torch.randint(wy, min(H, wy + 200), (4000,), generator=g).cuda()
+            xs = torch.randint(0, W, (4000,), generator=g).cuda()
+            m = mask[ys, xs] != 0
+            assert bool((L[ys, xs][~m] == -1).all()) and bool(torch.isnan(Cf[ys, xs][~m]).all())
+            yb, xb = ys[m], xs[m]
+            if yb.numel() == 0:
+                continue
+            f = (_blur64_rows(src, mean, yb, xb) - smu) * sinv
+            d = ((f[:, None, :] - Cn[None]) ** 2).sum(-1)
+            srt = torch.sort(d, dim=1).values
+            cid = (srt[:, 1] - srt[:, 0]) / srt[:, 1]
+            nbad += int(((L[yb, xb].long() != d.argmin(1)) & ~(cid < TAU)).sum())
+            worst = max(worst, float(((Cf[yb, xb].double() - cid).abs() / cid.abs().clamp(min=1.0)).max()))
+        assert nbad == 0, f"slide {s}: {nbad} sampled labels differ from the fp64 argmin"
+        assert worst < 1e-4, worst
