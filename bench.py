@@ -67,8 +67,8 @@ def parse():
     ap.add_argument("--source", default="auto", choices=["auto", "device", "synth", "host"],
                     help="where the raw slides live: device = resident in HBM before the timed "
                          "region; synth = not resident, generated band by band on the device "
-                         "inside the step (the stand-in for a slide reader); host = pinned host "
-                         "memory, streamed / uploaded by the residency policy inside the step; "
+                         "inside the step (the stand-in for a slide reader); host = page-locked "
+                         "host memory read band by band over PCIe inside the step; "
                          "auto = device when all fit in 60%% of HBM, else synth")
     ap.add_argument("--sweep", action="store_true",
                     help="time find_optimal_k (k=2..20) over the prepped rows instead of the "
@@ -95,18 +95,12 @@ class Slides:
                 self.items.append(D.synth_slide(H, W, C, seed=seed, mode=mode))
             elif source == "synth":
                 self.items.append(stream.SynthSource(H, W, C, seed, mode))
-            else:  # host: generated band by band on the device into pinned host memory
+            else:  # host: generated on the device into page-locked host chunks
                 src = stream.SynthSource(H, W, C, seed, mode)
-                host = stream.pinned_empty((H, W, C), torch.int16)
-                rows = max(1, (1 << 30) // (W * C * 2))
-                buf = torch.empty((rows, W, C), dtype=torch.int16, device="cuda")
-                for y0 in range(0, H, rows):
-                    y1 = min(H, y0 + rows)
-                    src.read(y0, y1, buf)
-                    host[y0:y1].copy_(buf[:y1 - y0])
-                del buf
-                mask = src.mask_device().cpu().numpy()
-                self.items.append((host.numpy().view(np.uint16), mask))
+                chunks = stream.pinned_rows(src, progress=lambda y: print(
+                    f"bench.py: slide {seed} in pinned host memory: {y}/{H} rows", file=sys.stderr,
+                    flush=True))
+                self.items.append((stream.HostSource(chunks), src.mask_device()))
         torch.cuda.synchronize()
 
     def images(self):
@@ -115,7 +109,7 @@ class Slides:
             return [M.img.from_device(raw, mask) for raw, mask in self.items]
         if self.source == "synth":
             return [M.img.from_source(src) for src in self.items]
-        return [M.img(a, mask=m) for a, m in self.items]
+        return [M.img.from_source(hs, mask=m) for hs, m in self.items]
 
 
 def make_step(slides, C, k, comm, sweep=False):

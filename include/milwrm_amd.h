@@ -94,6 +94,17 @@ size_t mw_mask_rank_ws_bytes(int64_t n_pix);
 int mw_mask_rank(const uint8_t* d_mask, int64_t n_pix, uint32_t* d_rank2pix,
                  int64_t* d_count, void* d_ws, void* stream);
 
+/* The same rank as a compact index (img.subsample_pixels' mask gather,
+ * MxIF.py:486-488, without a rank -> pixel table): per 64-pixel word its mask
+ * bits and the tissue pixels before it, per 64 ranks the word holding the
+ * first: mw_rank_index_bytes(n_pix) bytes (~n_pix / 6), d_count = M.  The *_ri
+ * forms below look a rank up in it (+ pix_off: the index of a slide band
+ * inside a larger array) -- the random lookups of a subsample then stay in
+ * the on-die caches instead of reading an HBM line per draw. */
+size_t mw_rank_index_bytes(int64_t n_pix);
+int mw_mask_rank_index(const uint8_t* d_mask, int64_t n_pix, void* d_index, int64_t* d_count, void* d_ws,
+                       void* stream);
+
 /* ---- subsample gather (MxIF.py:490-491) -------------------------------------
  * X[j, f] = img[rank2pix[idx[j]], feat[f]] as fp32 rows (S x F), plus per
  * block column statistics (count, mean, M2 in fp64) for StandardScaler.
@@ -102,6 +113,9 @@ size_t mw_gather_ws_bytes(int64_t S, int F);
 int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F,
                    const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S,
                    float* d_X, void* d_ws, void* stream);
+int mw_gather_rows_ri(const float* d_img, int C, const int32_t* d_feat, int F, const int32_t* d_idx,
+                      const void* d_index, int64_t n_pix, int64_t pix_off, int64_t S, float* d_X, void* d_ws,
+                      void* stream);
 /* Column statistics of rows already in X (same per-block records as
  * mw_gather_rows, same order: identical numbers for identical rows); then
  * mw_col_stats_finalize. */
@@ -130,6 +144,11 @@ int mw_blur_sample(const void* d_img, int dtype, int H, int W, int C, const floa
                    int64_t S, const int32_t* d_feat, int F, float* d_X, void* stream);
 int mw_sample_overflow(const int32_t* d_idx, const uint32_t* d_rank2pix, const int32_t* d_slots,
                        const int32_t* d_ovf, int64_t S, int F, float* d_X, void* stream);
+int mw_sample_map_ri(const int32_t* d_idx, const void* d_index, int64_t n_index, int64_t pix_off, int64_t S,
+                     int64_t n_pix, int32_t* d_slots, int32_t* d_ovf, void* stream);
+int mw_sample_overflow_ri(const int32_t* d_idx, const void* d_index, int64_t n_index, int64_t pix_off,
+                          const int32_t* d_slots, const int32_t* d_ovf, int64_t S, int F, float* d_X,
+                          void* stream);
 /* Row-window form for a slide streamed in row bands (img.subsample_pixels over a
  * slide that is not resident in HBM, MxIF.py:457-492): d_img holds the H rows
  * [row_off, row_off + H) of the slide (a band and its +-radius halo rows);
@@ -277,7 +296,7 @@ size_t mw_lloyd_ws_bytes(int64_t S, int k, int F);
 int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
                   const int32_t* d_qexp, int n, const mw_lloyd_fit* h_fits, int mode, int kind,
                   void* stream);
-/* per-column max |x| of S x F fp32 rows (F <= 256), fp32 out */
+/* per-column max |x| of S x F fp32 rows (F <= 16384), fp32 out */
 int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream);
 /* The same maxima folded into d_out (fp32 [F], >= 0) without resetting it:
  * the column maxima of a slide processed band after band. */

@@ -92,6 +92,11 @@ _PROTOS = {
                               c_vp, c_vp, c_vp]),
     "mw_blur_sample_rows": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i64, c_i32, c_i32, c_vp, c_f32, c_vp,
                                     c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
+    "mw_rank_index_bytes": (c_sz, [c_i64]),
+    "mw_mask_rank_index": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "mw_gather_rows_ri": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "mw_sample_map_ri": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "mw_sample_overflow_ri": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_slot_gather": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     "mw_blur_assign_rows": (c_i32, [c_vp, c_i32, c_i32, c_i32, c_i32, c_i64, c_i32, c_i32, c_vp, c_f32, c_vp,
                                     c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),

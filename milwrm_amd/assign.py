@@ -194,6 +194,11 @@ class _DomainSSE:
         y = xs + np.abs(pivot)
         self.exps = np.concatenate([_exp38((xs + cm) ** 2), _exp38(y), _exp38(y * y)]).astype(np.int32)
         self.pivot = pivot
+        # a non-finite value in a feature's column (maximum), its pivot or a
+        # center column has no fixed point: the reference's numpy sums give NaN
+        # there, so every quantity of that feature is NaN (conservatively: all
+        # domains of the feature, not only those holding the value)
+        self.nonfinite = ~(np.isfinite(xs) & np.isfinite(pivot) & np.isfinite(cm))
         self.chunks = [(d0, min(20, k - d0)) for d0 in range(0, k, 20)]
         self.feat_d, self.a_d, self.b_d, self.pv_d, self.qe_d = D.h2d_many(
             [np.asarray(feat, dtype=np.int32), inv, b, pivot, self.exps], dev)
@@ -237,7 +242,13 @@ class _DomainSSE:
             count[d0:d0 + kc] = o[4 * NQ:]
             if sums is None:
                 sums = (v[kc * F:kc * F + F], v[kc * F + F:])
-        return {"sse": sse, "sum": sums[0], "sumsq": sums[1], "count": count, "n": self.n,
+        s1, s2 = sums
+        if self.nonfinite.any():
+            sse[:, self.nonfinite] = np.nan
+            s1, s2 = s1.copy(), s2.copy()
+            s1[self.nonfinite] = np.nan
+            s2[self.nonfinite] = np.nan
+        return {"sse": sse, "sum": s1, "sumsq": s2, "count": count, "n": self.n,
                 "pivot": self.pivot}
 
 
@@ -274,7 +285,7 @@ def domain_sse_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarr
     lab = _labels_i8(tissue_id, n, k, dev)
     if pivot is None:
         pivot = _first_pixel_scaled(img_f32, feat, mu, inv)
-    if colmax is None:
+    if colmax is None:  # (mw_col_absmax takes up to 16384 channels)
         colmax = D.d2h(_colmax(img_f32))
     acc = _DomainSSE(feat, F, mu, inv, centers, pivot, colmax, dev)
     acc.add(img_f32, lab)

@@ -194,7 +194,8 @@ def prep_banded(image, batch, means, features, filter_name, sigma, fract, comm):
     if rows.shape[0]:
         feat = D.h2d(np.asarray(image._features(features), dtype=np.int32), dev)
         # pixel index of each band-row rank inside the local (halo'd) array
-        r2p_local = r2p + (b.y0 - b.lo) * W if b.y0 != b.lo else r2p
+        k = (b.y0 - b.lo) * W
+        r2p_local = (r2p.offset(k) if isinstance(r2p, D.RankIndex) else r2p + k) if k else r2p
         if not _gather_deferred(image, feat, local_idx, r2p_local, rows):
             src = D.as_float32(image._materialize())  # band + halo rows, blurred
             scratch = torch.zeros(1 + 2 * F, dtype=torch.float64, device=dev)

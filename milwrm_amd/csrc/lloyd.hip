@@ -139,11 +139,10 @@ constexpr int kList = 4;  // kQueue as two launches: lloyd_mark_kernel lists, th
 //   MODE 1: full E-step (labels updated) + inertia of the new labels
 //   MODE 2: inertia of the current labels
 template <int FMAX, int MODE, int KIND, int MBT>
-__global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict__ X, int64_t S, int F,
-                                                         const float* __restrict__ ga,
-                                                         const float* __restrict__ gb,
-                                                         const int* __restrict__ qexp,
-                                                         const LloydFitsArg fits, int n, int64_t R) {
+__device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int64_t S, int F,
+                                                const float* __restrict__ ga, const float* __restrict__ gb,
+                                                const int* __restrict__ qexp, const LloydFitsArg& fits, int n,
+                                                int64_t R) {
   constexpr int NV = FMAX / 4;
   constexpr int RP = 64 / FMAX;  // changed rows folded per M-step round (lane = row slot x feature)
   constexpr int NB = FMAX <= 16 ? 1 : FMAX / 16;  // 16-feature MFMA column blocks
@@ -630,6 +629,27 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
   }
 }
 
+template <int FMAX, int MODE, int KIND, int MBT>
+__global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict__ X, int64_t S, int F,
+                                                         const float* __restrict__ ga,
+                                                         const float* __restrict__ gb,
+                                                         const int* __restrict__ qexp,
+                                                         const LloydFitsArg fits, int n, int64_t R) {
+  lloyd_pass_body<FMAX, MODE, KIND, MBT>(X, S, F, ga, gb, qexp, fits, n, R);
+}
+// the first pass at F > 32 under a two-waves-per-SIMD register bound (the
+// unbounded instance holds 256 VGPRs + 33 AGPRs: one wave per SIMD; this one
+// 256 VGPRs and an 8-byte spill).  Config-5 cohort fit (2 x 40k^2 x 50
+// slides, same box, profiles/r04/bench_c5x2_synth*.json): 476.3 -> 460.4 ms.
+// The default; MW_LLOYD_FIRST_W2=0 takes the unbounded instance (same bits)
+__global__ void __launch_bounds__(256, 2) lloyd_first_w2_kernel(const float* __restrict__ X, int64_t S, int F,
+                                                               const float* __restrict__ ga,
+                                                               const float* __restrict__ gb,
+                                                               const int* __restrict__ qexp,
+                                                               const LloydFitsArg fits, int n, int64_t R) {
+  lloyd_pass_body<64, 0, kFirst, 1>(X, S, F, ga, gb, qexp, fits, n, R);
+}
+
 // kList, first launch: the bound test of every row of the block's range from
 // the row state alone (4 consecutive rows per lane, 4 groups of 256 rows per
 // wave in flight, no barrier until the end).  Decided rows get their drifted
@@ -738,8 +758,8 @@ __global__ void __launch_bounds__(256) lloyd_reduce_fits_kernel(const LloydFitsA
 // max; one LDS atomic per thread at the end.
 __global__ void __launch_bounds__(256) col_absmax_kernel(const float* __restrict__ X, int64_t S, int F,
                                                          unsigned* __restrict__ out) {
-  __shared__ unsigned s_m[256];
-  for (int f = threadIdx.x; f < 256; f += blockDim.x) s_m[f] = 0u;
+  extern __shared__ unsigned s_m[];  // F column maxima (dynamic: any F up to kColAbsMaxF)
+  for (int f = threadIdx.x; f < F; f += blockDim.x) s_m[f] = 0u;
   __syncthreads();
   const int64_t total = S * (int64_t)F;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // a multiple of F
@@ -759,6 +779,8 @@ __global__ void __launch_bounds__(256) col_absmax_kernel(const float* __restrict
   for (int q = threadIdx.x; q < F; q += blockDim.x) atomicMax(&out[q], s_m[q]);
 }
 
+constexpr int kColAbsMaxF = 16384;  // columns of col_absmax_kernel (F x 4 bytes of LDS)
+
 // grid of col_absmax_kernel: <= 2048 blocks, block count a multiple of F / gcd(256, F)
 static int col_absmax_blocks(int64_t total, int F) {
   int a = 256, b = F;
@@ -770,6 +792,8 @@ static int col_absmax_blocks(int64_t total, int F) {
 }
 
 }  // namespace mw
+
+#include "lloyd_dense.h"
 
 using namespace mw;
 
@@ -783,12 +807,13 @@ size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
 }
 
 int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream) {
-  MW_CHECK_ARG(d_X && d_out && S > 0 && F > 0 && F <= 256, "mw_col_absmax: bad arguments");
+  MW_CHECK_ARG(d_X && d_out && S > 0 && F > 0 && F <= kColAbsMaxF, "mw_col_absmax: bad arguments (F <= %d)",
+               kColAbsMaxF);
   hipStream_t s = as_stream(stream);
   MW_HIP(hipMemsetAsync(d_out, 0, sizeof(float) * F, s));
   const int64_t total = S * (int64_t)F;
   const int nb = col_absmax_blocks(total, F);
-  hipLaunchKernelGGL(col_absmax_kernel, dim3(nb), dim3(256), 0, s, d_X, S, F,
+  hipLaunchKernelGGL(col_absmax_kernel, dim3(nb), dim3(256), (size_t)F * sizeof(unsigned), s, d_X, S, F,
                      reinterpret_cast<unsigned*>(d_out));
   MW_LAUNCH_CHECK();
   return MW_OK;
@@ -797,11 +822,12 @@ int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream
 // max |x| per column folded into d_out (not reset first): a slide's column
 // maxima band after band (the exact QC sums take their fixed point from them)
 int mw_col_absmax_acc(const float* d_X, int64_t S, int F, float* d_out, void* stream) {
-  MW_CHECK_ARG(d_X && d_out && S > 0 && F > 0 && F <= 256, "mw_col_absmax_acc: bad arguments");
+  MW_CHECK_ARG(d_X && d_out && S > 0 && F > 0 && F <= kColAbsMaxF, "mw_col_absmax_acc: bad arguments (F <= %d)",
+               kColAbsMaxF);
   hipStream_t s = as_stream(stream);
   const int64_t total = S * (int64_t)F;
   const int nb = col_absmax_blocks(total, F);
-  hipLaunchKernelGGL(col_absmax_kernel, dim3(nb), dim3(256), 0, s, d_X, S, F,
+  hipLaunchKernelGGL(col_absmax_kernel, dim3(nb), dim3(256), (size_t)F * sizeof(unsigned), s, d_X, S, F,
                      reinterpret_cast<unsigned*>(d_out));
   MW_LAUNCH_CHECK();
   return MW_OK;
@@ -814,7 +840,7 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   MW_CHECK_ARG(S > 0 && F > 0 && n >= 1 && n <= kMaxFits, "mw_lloyd_pass: bad shape (1 <= n <= %d)",
                kMaxFits);
   MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_pass: bad mode %d", mode);
-  MW_CHECK_ARG(kind >= 0 && kind <= 4, "mw_lloyd_pass: bad kind %d", kind);
+  MW_CHECK_ARG(kind >= 0 && kind <= 6, "mw_lloyd_pass: bad kind %d", kind);
   if (mode != 0) kind = kFirst;  // modes 1 and 2 stream every tile
   if (kind == kList && S >= ((int64_t)1 << 31)) kind = kQueue;  // int32 row lists
   LloydFitsArg fits{};
@@ -834,6 +860,41 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   hipStream_t s = as_stream(stream);
   const int G = kblocks(S);
   const int64_t R = krows(S);
+  if (kind == kDense || kind == kDense + 1) {
+    // dense x . C^T pass over every fit of the launch (lloyd_dense.h); kind 6
+    // also writes the fits' distance bounds
+    DenseArg da{};
+    if (!dense_groups(h_fits, n, da)) {
+      set_error("mw_lloyd_pass: dense kind needs k <= %d per fit", kDenseMaxFitK);
+      return MW_EUNSUPPORTED;
+    }
+    MW_CHECK_ARG(kind == kDense || [&] {
+      for (int g = 0; g < n; ++g)
+        if (!h_fits[g].ub || !h_fits[g].lb) return false;
+      return true;
+    }(), "mw_lloyd_pass: kind 6 needs ub / lb");
+    da.bounds = kind == kDense ? 0 : (int)((1u << n) - 1u);
+    static const float bscale = [] {
+      const char* e = getenv("MW_DENSE_BSCALE");  // A/B of the recheck bound (never below the default)
+      const float v = e ? (float)atof(e) : kDenseBScale;
+      return v > kDenseBScale ? v : kDenseBScale;
+    }();
+    da.bscale = bscale;
+    da.G = G;
+    const dim3 gridd((unsigned)((G + 7) / 8 * 8) * (unsigned)da.ngroups);  // whole XCD rounds
+    if (F <= 32) {
+      hipLaunchKernelGGL(lloyd_dense_kernel<32>, gridd, dim3(256), dense_lds_bytes(32, F), s, d_X, S, F, d_a, d_b,
+                         d_qexp, fits, da, R);
+    } else {
+      hipLaunchKernelGGL(lloyd_dense_kernel<64>, gridd, dim3(256), dense_lds_bytes(64, F), s, d_X, S, F, d_a, d_b,
+                         d_qexp, fits, da, R);
+    }
+    MW_LAUNCH_CHECK();
+    const int rlmax = lloyd_rec(kmax, F);
+    hipLaunchKernelGGL(lloyd_reduce_fits_kernel, dim3((rlmax + 31) / 32, n), dim3(256), 0, s, fits, G, F);
+    MW_LAUNCH_CHECK();
+    return MW_OK;
+  }
   const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
   const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
   const dim3 grid((unsigned)G * (unsigned)n);
@@ -861,7 +922,13 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     else MW_LP(FMV, 0, kQueue, 1);                                              \
   } else if (mode == 1) MW_LP(FMV, 1, kFirst, 1);                               \
   else MW_LP(FMV, 2, kFirst, 1);
-  if (FM == 8) { MW_LPF(8) }
+  static const bool first_w2 = [] {
+    const char* e = getenv("MW_LLOYD_FIRST_W2");
+    return !(e && e[0] == '0');
+  }();
+  if (first_w2 && FM == 64 && mode == 0 && kind == kFirst && MBF == 1) {
+    hipLaunchKernelGGL(lloyd_first_w2_kernel, grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp, fits, n, R);
+  } else if (FM == 8) { MW_LPF(8) }
   else if (FM == 16) { MW_LPF(16) }
   else if (FM == 32) { MW_LPF(32) }
   else { MW_LPF(64) }

@@ -403,6 +403,114 @@ __global__ void __launch_bounds__(1024) mask_scan_kernel(uint32_t* __restrict__ 
   if (t == 1023) *count = (int64_t)s[1023];
 }
 
+// ------------------------------------------------------------ rank index
+// The mask rank as a compact index instead of a rank -> pixel table: per
+// 64-pixel word its mask bits (u64) and the tissue pixels before it (u32
+// prefix, one extra entry = M), and per 64 ranks the word holding the first
+// of them.  A lookup (rank_pixel) reads blk, one or two prefix entries and
+// one bit word, then selects the bit: ~1/6 byte of index per pixel (24 MB at
+// 10k^2 instead of a 340 MB table), so the random lookups of the subsample
+// hit the on-die caches instead of HBM lines.
+struct RankIndexPtrs {
+  const uint64_t* bits;
+  const uint32_t* pre;
+  const uint32_t* blk;
+};
+__host__ __device__ inline int64_t rank_words(int64_t n) { return (n + 63) / 64; }
+__host__ __device__ inline size_t rank_al(size_t x) { return (x + 255) & ~(size_t)255; }
+__host__ __device__ inline size_t rank_pre_off(int64_t n) { return rank_al((size_t)rank_words(n) * 8); }
+__host__ __device__ inline size_t rank_blk_off(int64_t n) {
+  return rank_pre_off(n) + rank_al((size_t)(rank_words(n) + 1) * 4);
+}
+__host__ __device__ inline size_t rank_index_bytes(int64_t n) {
+  return rank_blk_off(n) + rank_al((size_t)(rank_words(n) + 1) * 4);
+}
+__host__ __device__ inline RankIndexPtrs rank_ptrs(const void* base, int64_t n) {
+  const char* b = reinterpret_cast<const char*>(base);
+  return RankIndexPtrs{reinterpret_cast<const uint64_t*>(b), reinterpret_cast<const uint32_t*>(b + rank_pre_off(n)),
+                       reinterpret_cast<const uint32_t*>(b + rank_blk_off(n))};
+}
+// position of the r-th (0-based) set bit of m (r < popcount(m))
+__device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t r) {
+  uint32_t pos = 0;
+  uint32_t x = (uint32_t)m;
+  uint32_t c = __popc(x);
+  if (r >= c) { r -= c; pos = 32; x = (uint32_t)(m >> 32); }
+  c = __popc(x & 0xFFFFu);
+  if (r >= c) { r -= c; pos += 16; x >>= 16; }
+  c = __popc(x & 0xFFu);
+  if (r >= c) { r -= c; pos += 8; x >>= 8; }
+  c = __popc(x & 0xFu);
+  if (r >= c) { r -= c; pos += 4; x >>= 4; }
+  c = __popc(x & 0x3u);
+  if (r >= c) { r -= c; pos += 2; x >>= 2; }
+  c = x & 1u;
+  if (r >= c) pos += 1;
+  return pos;
+}
+// pixel of tissue rank rho (rho < M)
+__device__ __forceinline__ uint32_t rank_pixel(const RankIndexPtrs& ix, uint32_t rho) {
+  uint32_t w = ix.blk[rho >> 6];
+  uint32_t p0 = ix.pre[w], p1 = ix.pre[w + 1];
+  while (p1 <= rho) {
+    ++w;
+    p0 = p1;
+    p1 = ix.pre[w + 1];
+  }
+  return w * 64u + select64(ix.bits[w], rho - p0);
+}
+
+// per 64-pixel word: bits, prefix (block base from mask_scan_kernel + the
+// block's own scan), and blk[] for the ranks 64b that fall in the word
+__global__ void __launch_bounds__(256) rank_words_kernel(const uint8_t* __restrict__ m, int64_t n,
+                                                         const uint32_t* __restrict__ base,
+                                                         const int64_t* __restrict__ count,
+                                                         uint64_t* __restrict__ bits, uint32_t* __restrict__ pre,
+                                                         uint32_t* __restrict__ blk) {
+  __shared__ uint32_t s_w[4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int64_t NW = rank_words(n);
+  const int64_t w = (int64_t)blockIdx.x * (kMaskChunk / 64) + t;  // 256 words per block
+  const int64_t p = w * 64;
+  uint64_t b = 0;
+  if (p + 64 <= n) {
+    const uint4* v4 = reinterpret_cast<const uint4*>(m + p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint4 v = v4[j];
+      const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          b |= ((ww[k] >> (8 * q)) & 0xFFu) ? 1ull << (16 * j + 4 * k + q) : 0ull;
+    }
+  } else if (p < n) {
+    for (int q = 0; q < 64 && p + q < n; ++q) b |= m[p + q] ? 1ull << q : 0ull;
+  }
+  const uint32_t c = __popcll(b);
+  uint32_t incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t wbase = base[blockIdx.x];
+  for (int j = 0; j < wid; ++j) wbase += s_w[j];
+  const uint32_t lo = wbase + incl - c;
+  if (w < NW) {
+    bits[w] = b;
+    pre[w] = lo;
+    for (uint32_t r = (lo + 63) & ~63u; r < lo + c; r += 64) blk[r >> 6] = (uint32_t)w;
+  }
+  if (w == NW - 1) {
+    pre[NW] = (uint32_t)*count;
+    if (((uint32_t)*count & 63u) == 0) blk[(uint32_t)*count >> 6] = (uint32_t)NW;  // sentinel (never read for rho < M)
+  }
+}
+
 __global__ void __launch_bounds__(256) mask_scatter_kernel(const uint8_t* __restrict__ m, int64_t n,
                                                            const uint32_t* __restrict__ base,
                                                            uint32_t* __restrict__ r2p) {
@@ -473,13 +581,20 @@ __device__ __forceinline__ void chan_merge(double& n_a, double& m_a, double& q_a
 // GATHER false: the rows are already in X (written by the fused blur sample
 // epilogue) and only the statistics are taken, over the same block/tile
 // partition and in the same order, so both give identical records.
-template <bool GATHER>
+// RI: the sample -> pixel lookups through the rank index (rank_pixel, + pix_off)
+// instead of the rank -> pixel table r2p
+template <bool GATHER, bool RI = false>
 __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ img, int C,
                                                      const int32_t* __restrict__ feat, int F,
                                                      const int32_t* __restrict__ idx,
                                                      const uint32_t* __restrict__ r2p, int64_t S,
                                                      int64_t R, float* __restrict__ X,
-                                                     double* __restrict__ rec) {
+                                                     double* __restrict__ rec, RankIndexPtrs ix = {},
+                                                     int64_t pix_off = 0) {
+  auto pix_of = [&](int32_t rho) -> uint32_t {
+    if constexpr (RI) return rank_pixel(ix, (uint32_t)rho) + (uint32_t)pix_off;
+    else return r2p[rho];
+  };
   extern __shared__ __attribute__((aligned(16))) float s_tile[];  // 256*F floats + stats scratch
   __shared__ int s_feat[64];
   __shared__ uint32_t s_pix[2][256];  // pixel of each row of this tile / the next one
@@ -500,7 +615,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
   const int fcol = lf < F ? (GATHER ? s_feat[lf] : lf) : 0;
   // the sample -> pixel lookups (idx, then r2p: two dependent random reads)
   // of tile i+1 are issued before tile i's row loads and stored after them
-  if (GATHER && lo < hi && t < (int)min((int64_t)kTile, hi - lo)) s_pix[0][t] = r2p[idx[lo + t]];
+  if (GATHER && lo < hi && t < (int)min((int64_t)kTile, hi - lo)) s_pix[0][t] = pix_of(idx[lo + t]);
   int buf = 0;
   for (int64_t r0 = lo; r0 < hi; r0 += kTile, buf ^= 1) {
     const int nrow = (int)min((int64_t)kTile, hi - r0);
@@ -515,7 +630,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
     bool npix_issued = false;
     for (int i0 = 0; i0 < 64 / RPI; i0 += kBatch) {
       if (i0 == kBatch && nxt) {  // nidx has landed with the first batch of rows
-        npix = r2p[nidx];
+        npix = pix_of(nidx);
         npix_issued = true;
       }
       float v[kBatch];
@@ -530,7 +645,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
         if (i0 + i < 64 / RPI && row < nrow && lf < F) s_tile[row * F + lf] = v[i];
       }
     }
-    if (nxt) s_pix[buf ^ 1][t] = npix_issued ? npix : r2p[nidx];
+    if (nxt) s_pix[buf ^ 1][t] = npix_issued ? npix : pix_of(nidx);
     __syncthreads();
     // coalesced write of the tile (rows contiguous in X)
     if (GATHER) {
@@ -938,6 +1053,45 @@ int mw_mask_rank(const uint8_t* d_mask, int64_t n_pix, uint32_t* d_rank2pix, int
   return MW_OK;
 }
 
+size_t mw_rank_index_bytes(int64_t n_pix) { return rank_index_bytes(n_pix); }
+
+int mw_mask_rank_index(const uint8_t* d_mask, int64_t n_pix, void* d_index, int64_t* d_count, void* d_ws,
+                       void* stream) {
+  MW_CHECK_ARG(d_mask && d_index && d_count && d_ws, "mw_mask_rank_index: null pointer");
+  MW_CHECK_ARG(n_pix > 0 && n_pix < (int64_t)4294967295LL - 64, "mw_mask_rank_index: n_pix out of range");
+  MW_CHECK_ARG(((uintptr_t)d_mask & 15) == 0, "mw_mask_rank_index: mask must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const int nb = (int)((n_pix + kMaskChunk - 1) / kMaskChunk);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(d_ws);
+  hipLaunchKernelGGL(mask_count_kernel, dim3(nb), dim3(256), 0, st, d_mask, n_pix, cnt);
+  MW_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mask_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, nb, d_count);
+  MW_LAUNCH_CHECK();
+  char* b = reinterpret_cast<char*>(d_index);
+  hipLaunchKernelGGL(rank_words_kernel, dim3(nb), dim3(256), 0, st, d_mask, n_pix, cnt, d_count,
+                     reinterpret_cast<uint64_t*>(b), reinterpret_cast<uint32_t*>(b + rank_pre_off(n_pix)),
+                     reinterpret_cast<uint32_t*>(b + rank_blk_off(n_pix)));
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_gather_rows_ri(const float* d_img, int C, const int32_t* d_feat, int F, const int32_t* d_idx,
+                      const void* d_index, int64_t n_pix, int64_t pix_off, int64_t S, float* d_X, void* d_ws,
+                      void* stream) {
+  MW_CHECK_ARG(d_img && d_feat && d_idx && d_index && d_X && d_ws, "mw_gather_rows_ri: null pointer");
+  MW_CHECK_ARG(S > 0 && F > 0 && F <= 64 && C > 0 && n_pix > 0 && pix_off >= 0,
+               "mw_gather_rows_ri: bad shape S=%lld F=%d", (long long)S, F);
+  hipStream_t st = as_stream(stream);
+  const int G = stream_blocks(S);
+  const int64_t R = rows_per_block(S);
+  size_t lds = (size_t)kTile * F * sizeof(float);
+  if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
+  hipLaunchKernelGGL((gather_kernel<true, true>), dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_idx,
+                     nullptr, S, R, d_X, reinterpret_cast<double*>(d_ws), rank_ptrs(d_index, n_pix), pix_off);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
 size_t mw_gather_ws_bytes(int64_t S, int F) {
   return (size_t)stream_blocks(S) * (1 + 3 * (size_t)F) * sizeof(double) + 256;
 }
@@ -952,8 +1106,8 @@ int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F, cons
   const int64_t R = rows_per_block(S);
   size_t lds = (size_t)kTile * F * sizeof(float);
   if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
-  hipLaunchKernelGGL(gather_kernel<true>, dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_idx,
-                     d_rank2pix, S, R, d_X, reinterpret_cast<double*>(d_ws));
+  hipLaunchKernelGGL((gather_kernel<true, false>), dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_idx,
+                     d_rank2pix, S, R, d_X, reinterpret_cast<double*>(d_ws), RankIndexPtrs{}, (int64_t)0);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
@@ -976,31 +1130,43 @@ int mw_col_stats_rows(const float* d_X, int64_t S, int F, void* d_ws, void* stre
 // (both read from the side data, no dependent load); mw_sample_overflow then
 // copies row j0 to the overflow slots.  Which draw lands in which place
 // depends on the atomic order, the rows written do not.
+extern "C++" {
+template <bool RI = false>
 __global__ void __launch_bounds__(256) sample_map_kernel(const int32_t* __restrict__ idx,
                                                          const uint32_t* __restrict__ r2p, int64_t S,
                                                          int32_t* __restrict__ slots,
-                                                         int32_t* __restrict__ ovf) {
+                                                         int32_t* __restrict__ ovf, RankIndexPtrs ix = {},
+                                                         int64_t pix_off = 0) {
   for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < S; j += (int64_t)gridDim.x * 256) {
-    const uint32_t p = r2p[idx[j]];
+    uint32_t p;
+    if constexpr (RI) p = rank_pixel(ix, (uint32_t)idx[j]) + (uint32_t)pix_off;
+    else p = r2p[idx[j]];
     if (atomicCAS(slots + 2 * (int64_t)p, -1, (int32_t)j) == -1) continue;
     if (atomicCAS(slots + 2 * (int64_t)p + 1, -1, (int32_t)j) == -1) continue;
     ovf[1 + atomicAdd(ovf, 1)] = (int32_t)j;
   }
 }
+template <bool RI = false>
 __global__ void __launch_bounds__(256) sample_overflow_kernel(const int32_t* __restrict__ idx,
                                                               const uint32_t* __restrict__ r2p,
                                                               const int32_t* __restrict__ slots,
                                                               const int32_t* __restrict__ ovf, int F,
-                                                              float* __restrict__ X) {
+                                                              float* __restrict__ X, RankIndexPtrs ix = {},
+                                                              int64_t pix_off = 0) {
   const int n = ovf[0];
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int32_t j = ovf[1 + i];
-    const int32_t h = slots[2 * (int64_t)r2p[idx[j]]];
+    uint32_t p;
+    if constexpr (RI) p = rank_pixel(ix, (uint32_t)idx[j]) + (uint32_t)pix_off;
+    else p = r2p[idx[j]];
+    const int32_t h = slots[2 * (int64_t)p];
     const float* src = X + (int64_t)h * F;
     float* dst = X + (int64_t)j * F;
     for (int f = 0; f < F; ++f) dst[f] = src[f];
   }
 }
+
+}  // extern "C++"
 
 // The sample epilogue as a pass of its own over a materialised fp32 band of
 // n pixels (slide pixels pix_off ..): X[j] = band[p - pix_off, feat] for both
@@ -1049,7 +1215,36 @@ int mw_sample_map(const int32_t* d_idx, const uint32_t* d_rank2pix, int64_t S, i
   MW_HIP(hipMemsetAsync(d_slots, 0xff, mw_sample_slot_elems(n_pix) * sizeof(int32_t), st));
   MW_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), st));
   const int grid = (int)std::min<int64_t>((S + 255) / 256, 8192);
-  hipLaunchKernelGGL(sample_map_kernel, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, S, d_slots, d_ovf);
+  hipLaunchKernelGGL(sample_map_kernel<false>, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, S, d_slots, d_ovf,
+                     RankIndexPtrs{}, (int64_t)0);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_sample_map_ri(const int32_t* d_idx, const void* d_index, int64_t n_index, int64_t pix_off, int64_t S,
+                     int64_t n_pix, int32_t* d_slots, int32_t* d_ovf, void* stream) {
+  MW_CHECK_ARG(d_idx && d_index && d_slots && d_ovf, "mw_sample_map_ri: null pointer");
+  MW_CHECK_ARG(S > 0 && S < 0x7fffffffll && n_pix > 0 && n_index > 0 && pix_off >= 0,
+               "mw_sample_map_ri: bad sizes S=%lld n_pix=%lld", (long long)S, (long long)n_pix);
+  hipStream_t st = as_stream(stream);
+  MW_HIP(hipMemsetAsync(d_slots, 0xff, mw_sample_slot_elems(n_pix) * sizeof(int32_t), st));
+  MW_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), st));
+  const int grid = (int)std::min<int64_t>((S + 255) / 256, 8192);
+  hipLaunchKernelGGL(sample_map_kernel<true>, dim3(grid), dim3(256), 0, st, d_idx, nullptr, S, d_slots, d_ovf,
+                     rank_ptrs(d_index, n_index), pix_off);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_sample_overflow_ri(const int32_t* d_idx, const void* d_index, int64_t n_index, int64_t pix_off,
+                          const int32_t* d_slots, const int32_t* d_ovf, int64_t S, int F, float* d_X,
+                          void* stream) {
+  MW_CHECK_ARG(d_idx && d_index && d_slots && d_ovf && d_X && S > 0 && F > 0 && n_index > 0,
+               "mw_sample_overflow_ri: bad args");
+  hipStream_t st = as_stream(stream);
+  const int grid = (int)std::min<int64_t>((S / 64 + 255) / 256 + 1, 1024);
+  hipLaunchKernelGGL(sample_overflow_kernel<true>, dim3(grid), dim3(256), 0, st, d_idx, nullptr, d_slots, d_ovf,
+                     F, d_X, rank_ptrs(d_index, n_index), pix_off);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }
@@ -1060,8 +1255,8 @@ int mw_sample_overflow(const int32_t* d_idx, const uint32_t* d_rank2pix, const i
                "mw_sample_overflow: bad args");
   hipStream_t st = as_stream(stream);
   const int grid = (int)std::min<int64_t>((S / 64 + 255) / 256 + 1, 1024);
-  hipLaunchKernelGGL(sample_overflow_kernel, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, d_slots, d_ovf,
-                     F, d_X);
+  hipLaunchKernelGGL(sample_overflow_kernel<false>, dim3(grid), dim3(256), 0, st, d_idx, d_rank2pix, d_slots,
+                     d_ovf, F, d_X, RankIndexPtrs{}, (int64_t)0);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

@@ -266,15 +266,47 @@ def block_mean(img: torch.Tensor, fact: int):
     return out
 
 
+class RankIndex:
+    """The mask rank of a slide as the compact index of mw_mask_rank_index
+    (per 64-pixel word: mask bits and the tissue pixels before it; ~n/6
+    bytes): the kernels map a tissue rank to its pixel through it (+
+    ``pix_off``, the pixel offset of a band inside a larger array)."""
+
+    def __init__(self, buf: torch.Tensor, n_pix: int, pix_off: int = 0):
+        self.buf, self.n_pix, self.pix_off = buf, int(n_pix), int(pix_off)
+
+    def offset(self, k: int) -> "RankIndex":
+        return RankIndex(self.buf, self.n_pix, self.pix_off + int(k))
+
+    def __getitem__(self, sl):  # r2p[:M] of the table form: the index covers every rank
+        return self
+
+
+# The rank -> pixel table (mw_mask_rank, 4 bytes per tissue pixel: one lookup
+# per draw, the faster gather -- config 2: 1.67 vs 1.81 ms) for slides up to
+# RANK_TABLE_MAX_PIX pixels (1 GiB of table); the compact index above (config
+# 5's 40k x 40k slide: 0.27 GB instead of 6.4 GB).  MW_RANK_TABLE=1 / 0 forces
+# the table / the index.
+_RT = os.environ.get("MW_RANK_TABLE")
+RANK_TABLE_MAX_PIX = (1 << 62) if _RT == "1" else 0 if _RT == "0" else (1 << 28)
+
+
 def mask_rank_async(mask_u8: torch.Tensor):
-    """Launch the mask rank (no host sync): (rank→pixel int32 tensor of
-    length n, device count of mask != 0)."""
+    """Launch the mask rank (no host sync): (the rank→pixel int32 table of
+    length n -- a RankIndex above RANK_TABLE_MAX_PIX pixels --, device count
+    of mask != 0)."""
     n = mask_u8.numel()
-    r2p = torch.empty(n, dtype=torch.int32, device=mask_u8.device)
     cnt = torch.empty(1, dtype=torch.int64, device=mask_u8.device)
     ws = WS.get("mrank", N.query("mw_mask_rank_ws_bytes", n))
-    with profiling.timed("mask_rank", n):
-        N.call("mw_mask_rank", P(mask_u8), n, P(r2p), P(cnt), P(ws), stream())
+    if n <= RANK_TABLE_MAX_PIX:
+        r2p = torch.empty(n, dtype=torch.int32, device=mask_u8.device)
+        with profiling.timed("mask_rank", n):
+            N.call("mw_mask_rank", P(mask_u8), n, P(r2p), P(cnt), P(ws), stream())
+    else:
+        buf = torch.empty(N.query("mw_rank_index_bytes", n), dtype=torch.uint8, device=mask_u8.device)
+        with profiling.timed("mask_rank", n):
+            N.call("mw_mask_rank_index", P(mask_u8), n, P(buf), P(cnt), P(ws), stream())
+        r2p = RankIndex(buf, n)
     # the count comes back by its own copy and event, so reading it later
     # does not wait for work queued after the rank (e.g. the blur)
     slot = _PINNED.take(8)
@@ -287,8 +319,9 @@ def mask_rank_async(mask_u8: torch.Tensor):
 
 
 def mask_rank(mask_u8: torch.Tensor, pending=None):
-    """(rank→pixel int32 tensor of length M, M) for mask != 0 (row-major);
-    ``pending`` = an earlier mask_rank_async result for the same mask."""
+    """(RankIndex or rank→pixel int32 tensor of length M, M) for mask != 0
+    (row-major); ``pending`` = an earlier mask_rank_async result for the same
+    mask."""
     r2p, cnt, (slot, hv, ev) = mask_rank_async(mask_u8) if pending is None else pending
     ev.synchronize()
     M = int(hv[0])
@@ -307,8 +340,12 @@ def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2
         return
     ws = WS.get("gather", N.query("mw_gather_ws_bytes", S, F))
     with profiling.timed("gather", S * (F * 4 * 2 + 8)):
-        N.call("mw_gather_rows", P(img_f32), C, P(feat), F, P(idx), P(r2p), S, P(X_out), P(ws),
-               stream())
+        if isinstance(r2p, RankIndex):
+            N.call("mw_gather_rows_ri", P(img_f32), C, P(feat), F, P(idx), P(r2p.buf), r2p.n_pix, r2p.pix_off,
+                   S, P(X_out), P(ws), stream())
+        else:
+            N.call("mw_gather_rows", P(img_f32), C, P(feat), F, P(idx), P(r2p), S, P(X_out), P(ws),
+                   stream())
     N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
     if absmax is not None:
         N.call("mw_col_stats_absmax", P(ws), S, F, P(absmax), 1, stream())

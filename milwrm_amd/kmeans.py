@@ -316,6 +316,7 @@ class _FitState:
         self.iexp = 0
         self.drift_max = 0.0
         self.prev_dmax = 0.0
+        self.bounds_ok = True  # ub / lb hold valid bounds (a dense pass does not keep them)
 
     def add(self, rec, F, qscale, a64, b64):
         """Apply a pass's record (mode 0): exact sums, sizes; returns the
@@ -337,7 +338,13 @@ class _FitState:
         return a64[None, :] * sums_x + b64[None, :] * cnt[:, None], cnt, tail[0]
 
 
-KIND_FIRST, KIND_TILE, KIND_QUEUE, KIND_LIST = 0, 1, 2, 4
+KIND_FIRST, KIND_TILE, KIND_QUEUE, KIND_LIST, KIND_DENSE = 0, 1, 2, 4, 5
+# the batched sweep's dense pass (lloyd_dense.h: x . C^T of every fit in the
+# launch on the matrix cores, exact fp32 recheck of near ties) while at least
+# this many fits run together; fewer -> the bounded passes (MW_LLOYD_DENSE=0:
+# never)
+DENSE_MIN_FITS = int(os.environ.get("MW_LLOYD_DENSE_MIN", "3"))
+USE_DENSE = os.environ.get("MW_LLOYD_DENSE", "1") != "0"
 # the few-undecided pass: kList (bound test and list in one launch, the listed
 # rows in a second) unless MW_LLOYD_LIST=0 (kQueue: both phases chunk by chunk
 # in one kernel)
@@ -365,8 +372,11 @@ def _launch_pass(rows, fits_g, mode, kind, par, poff, outs, st, label="lloyd_pas
         arr[i] = N.LloydFit(base, base + k * F * 4, base + (k * F + k) * 4, D.P(fs.labels),
                             D.P(fs.ub), D.P(fs.lb), D.P(fs.ws), D.P(outs[g]), k,
                             float(fs.drift_max), int(fs.iexp))
-        nbytes += S * 9 + (S * F * 4 if (mode or kind not in (KIND_QUEUE, KIND_LIST)) else 0)
-    tag = "" if mode else ("_first", "_tile", "_queue", "_first_atomic", "_list")[kind]
+        if kind == KIND_DENSE:  # rows once per launch (counted with the first fit), labels per fit
+            nbytes += 2 * S + (S * F * 4 if i == 0 else 0)
+        else:
+            nbytes += S * 9 + (S * F * 4 if (mode or kind not in (KIND_QUEUE, KIND_LIST)) else 0)
+    tag = "" if mode else ("_first", "_tile", "_queue", "_first_atomic", "_list", "_dense", "_dense")[kind]
     ev = None
     if TRACE is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -426,6 +436,8 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
             k = fs.k
             c32 = fs.centers.astype(np.float32)
             drift, dmax, half = _bound_tables(c32, fs.prev32)
+            if not fs.bounds_ok:  # after dense passes: every row recomputed, bounds rewritten
+                drift, dmax = np.full(k, np.inf, np.float32), float("inf")
             fs.prev_dmax = fs.drift_max if fs.prev32 is not None else 0.0
             fs.prev32, fs.drift_max = c32, dmax
             o = int(poff[g])
@@ -447,14 +459,20 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
 
     first = 3 if os.environ.get("MW_LLOYD_FIRST_ATOMIC") == "1" else KIND_FIRST
 
+    dense_now = [False]
+
     def kind_of(g):
-        """First pass, then kTile or kQueue by the predicted share of
-        undecided rows: the last pass's share scaled by how far the centers
-        moved now relative to then (rows fail the bound test about in
-        proportion to the drift)."""
+        """First pass; then the dense pass while enough fits run together;
+        else kTile or kQueue by the predicted share of undecided rows: the
+        last pass's share scaled by how far the centers moved now relative to
+        then (rows fail the bound test about in proportion to the drift)."""
         fs = fits[g]
         if not fs.history:
             return first
+        if dense_now[0]:
+            return KIND_DENSE
+        if not fs.bounds_ok:
+            return KIND_TILE
         frac = fs.history[-1][1] / max(S_glob, 1)
         if fs.prev_dmax > 0 and np.isfinite(fs.drift_max):
             frac *= min(1.0, fs.drift_max / fs.prev_dmax)
@@ -464,14 +482,18 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
     if comm.sharded():
         S_glob = int(comm.all_gather_np(np.array([S], dtype=np.int64))[:, 0].sum())
 
+    dense_ok = USE_DENSE and F <= 64 and max(ks) <= 20  # lloyd_dense.h kDenseMaxFitK
     for it in range(max_iter):
         active = [g for g in range(n) if not fits[g].done]
         if not active:
             break
+        dense_now[0] = dense_ok and it > 0 and len(active) >= DENSE_MIN_FITS
         upload(active)
         rec_all = run(active, 0, kind_of)
         for g in active:
             fs = fits[g]
+            if it > 0:
+                fs.bounds_ok = not dense_now[0]
             sums, weight, changed = fs.add(rec_all[roff[g]:roff[g + 1]], F, qscale, a64, b64)
             centers_new = sums.copy()
             _relocate_empty(rows, fs.labels, fs.centers, centers_new, weight, comm)

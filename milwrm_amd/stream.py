@@ -195,12 +195,22 @@ class DeviceSource(RowSource):
 
 
 class HostSource(RowSource):
-    """A slide in host memory (numpy array or CPU tensor, HWC or HW)."""
+    """A slide in host memory: a numpy array or CPU tensor (HWC or HW), or a
+    list of CPU tensors holding consecutive row ranges (e.g. page-locked
+    chunks, ``pinned_rows``)."""
 
     kind = "host"
 
     def __init__(self, arr):
-        if isinstance(arr, torch.Tensor):
+        self._chunks = None
+        if isinstance(arr, (list, tuple)):
+            self._chunks = [t if t.dim() == 3 else t[:, :, None] for t in arr]
+            self.H = sum(int(t.shape[0]) for t in self._chunks)
+            _, self.W, self.C = (int(x) for x in self._chunks[0].shape)
+            self.dtype = self._chunks[0].dtype
+            self._starts = np.cumsum([0] + [int(t.shape[0]) for t in self._chunks])
+            self._t = self._a = None
+        elif isinstance(arr, torch.Tensor):
             t = arr if arr.dim() == 3 else arr[:, :, None]
             self.H, self.W, self.C = (int(x) for x in t.shape)
             self.dtype = t.dtype
@@ -226,8 +236,14 @@ class HostSource(RowSource):
         return torch.from_numpy(np.ascontiguousarray(a))
 
     def read(self, y0, y1, out):
-        h = self._host_rows(y0, y1)
         dst = out[:y1 - y0]
+        if self._chunks is not None:
+            for i, t in enumerate(self._chunks):
+                a, b = max(y0, int(self._starts[i])), min(y1, int(self._starts[i + 1]))
+                if a < b:
+                    dst[a - y0:b - y0].copy_(t[a - self._starts[i]:b - self._starts[i]], non_blocking=True)
+            return dst
+        h = self._host_rows(y0, y1)
         dst.copy_(h, non_blocking=True)
         if not h.is_pinned():
             self._keep = [h]  # (a pageable copy is staged by the runtime before it returns)
@@ -238,6 +254,22 @@ def pinned_empty(shape, dtype=torch.int16) -> torch.Tensor:
     """Page-locked host tensor: bands of a HostSource over it are copied by
     DMA without a staging copy."""
     return torch.empty(shape, dtype=dtype, pin_memory=True)
+
+
+def pinned_rows(src: RowSource, chunk_bytes: int = 1 << 30, progress=None) -> list:
+    """The rows of ``src`` copied into page-locked host chunks of about
+    ``chunk_bytes`` (a ``HostSource`` over the list reads them back by DMA)."""
+    rows = max(1, chunk_bytes // src.row_bytes)
+    buf = torch.empty((min(rows, src.H), src.W, src.C), dtype=src.dtype, device=D.device())
+    out = []
+    for y0 in range(0, src.H, rows):
+        y1 = min(src.H, y0 + rows)
+        h = torch.empty((y1 - y0, src.W, src.C), dtype=src.dtype, pin_memory=True)
+        h.copy_(src.read(y0, y1, buf))
+        out.append(h)
+        if progress:
+            progress(y1)
+    return out
 
 
 def _synth_params(H, W, C, seed, mode="hard", n_seeds=32, n_domains=8, bg_frac=0.15):
@@ -379,8 +411,9 @@ def nz_stats(src: RowSource):
 
 
 def blur_gather(src, sigma: float, inv_mean, pseudoval: float, feat: torch.Tensor, idx: torch.Tensor,
-                r2p: torch.Tensor, X_out: torch.Tensor, truncate: float = 4.0, band_rows=None) -> bool:
-    """X_out[j] = blur(lognorm(slide))[r2p[idx[j]], feat] without storing the
+                r2p, X_out: torch.Tensor, truncate: float = 4.0, band_rows=None) -> bool:
+    """X_out[j] = blur(lognorm(slide))[pixel of rank idx[j], feat] (``r2p``: a
+    device.RankIndex or a rank -> pixel table) without storing the
     blurred slide (``img.subsample_pixels`` after a deferred blur,
     MxIF.py:457-492): the sample map (per pixel its first two sample slots,
     later draws on an overflow list), then per band the blur with its sample
@@ -399,8 +432,13 @@ def blur_gather(src, sigma: float, inv_mean, pseudoval: float, feat: torch.Tenso
     slots = D.WS.get("sample_slots", 4 * N.query("mw_sample_slot_elems", n))
     ovf = D.WS.get("sample_ovf", 4 * (S + 1))
     st = D.stream()
+    ri = isinstance(r2p, D.RankIndex)
     with profiling.timed("sample_map", S * 16):
-        N.call("mw_sample_map", D.P(idx), D.P(r2p), S, n, D.P(slots), D.P(ovf), st)
+        if ri:
+            N.call("mw_sample_map_ri", D.P(idx), D.P(r2p.buf), r2p.n_pix, r2p.pix_off, S, n, D.P(slots),
+                   D.P(ovf), st)
+        else:
+            N.call("mw_sample_map", D.P(idx), D.P(r2p), S, n, D.P(slots), D.P(ovf), st)
     elem = torch.empty(0, dtype=src.dtype).element_size()
     if band_rows is None:
         band_rows = H if src.zero_copy else band_rows_for(src)
@@ -426,7 +464,11 @@ def blur_gather(src, sigma: float, inv_mean, pseudoval: float, feat: torch.Tenso
             N.call("mw_slot_gather", D.P(core), C, (y1 - y0) * W, y0 * W, D.P(slots), S, D.P(feat), F,
                    D.P(X_out), D.stream())
     with profiling.timed("sample_overflow", 0):
-        N.call("mw_sample_overflow", D.P(idx), D.P(r2p), D.P(slots), D.P(ovf), S, F, D.P(X_out), D.stream())
+        if ri:
+            N.call("mw_sample_overflow_ri", D.P(idx), D.P(r2p.buf), r2p.n_pix, r2p.pix_off, D.P(slots), D.P(ovf),
+                   S, F, D.P(X_out), D.stream())
+        else:
+            N.call("mw_sample_overflow", D.P(idx), D.P(r2p), D.P(slots), D.P(ovf), S, F, D.P(X_out), D.stream())
     D.FUSED_USED["sample"] += 1
     if not src.zero_copy:
         D.FUSED_USED["sample_streamed"] += 1

@@ -105,8 +105,9 @@ def test_config3_config4_two_ranks_full_size(gpu):
     assert ref["S"] == got[0]["S"] + got[1]["S"] > 1.3e8
     for r in (0, 1):
         g = got[r]
-        for key in ("mean", "scale", "idx", "centers", "curve", "conf_df"):
+        for key in ("mean", "scale", "idx", "centers", "curve"):
             np.testing.assert_array_equal(g[key], ref[key], err_msg=key)
+        np.testing.assert_array_equal(g["conf_df"], ref["conf_df"][r:r + 1])  # this rank's slide
         assert g["n_iter"] == ref["n_iter"]
         assert g["inertia"] == ref["inertia"]
         assert g["best_k"] == ref["best_k"]

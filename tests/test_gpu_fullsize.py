@@ -130,6 +130,12 @@ def _check_label_pass(raw, mask, lab, mean, smu, sinv, n=100_000, seed=0, step=5
     assert worst < RTOL, worst
 
 
+def _label_sums(labels, xs, k):
+    """Per-label fp64 sums of the rows (a one-hot GEMM: no atomics)."""
+    onehot = torch.nn.functional.one_hot(labels, k).double()
+    return onehot.T @ xs
+
+
 def _lloyd64(lab, smu, sinv, step=2_000_000):
     """Test infrastructure: sklearn's ``_kmeans_single_lloyd`` (_kmeans.py:
     624-752, as oracle.lloyd) in fp64 torch on the device, from the fit's own
@@ -159,12 +165,13 @@ def _lloyd64(lab, smu, sinv, step=2_000_000):
             if want_gap:
                 top = torch.topk(d, 2, dim=1, largest=False).values
                 gap[a:b] = (top[:, 1] - top[:, 0]) / top[:, 1]
-            sums.index_add_(0, lab_[a:b], xs)
+            sums += _label_sums(lab_[a:b], xs, k)
         cnt = torch.bincount(lab_, minlength=k).double()
         return lab_, sums, cnt, gap
 
     strict = False
     for it in range(km.max_iter):
+        print(f"fp64 Lloyd iteration {it}", flush=True)
         labels, sums, cnt, _ = estep(centers)
         assert bool((cnt > 0).all()), "empty cluster: relocation is outside this check"
         new = sums / cnt[:, None]
@@ -204,7 +211,7 @@ def _check_centers_are_means(lab, smu, sinv, step=2_000_000):
     labels = km._labels_dev.long()
     sums = torch.zeros((k, F), dtype=torch.float64, device=rows.X.device)
     for a, b in _chunks(S, step):
-        sums.index_add_(0, labels[a:b], (rows.X[a:b].double() - smu) * sinv)
+        sums += _label_sums(labels[a:b], (rows.X[a:b].double() - smu) * sinv, k)
     cnt = torch.bincount(labels, minlength=k).double()
     means = (sums / cnt[:, None]).cpu().numpy()
     c = km.cluster_centers_

@@ -1,7 +1,14 @@
 """Lloyd pass kinds are exact: with every bounded pass forced to kTile, or to
 kQueue, or to kList (twice), or the default mix, the fits equal the plain Lloyd E-step every pass
 (MW_LLOYD_NOBOUND) bit for bit — labels, centers, n_iter — for k = 8..20 in
-one batched launch, and repeated runs agree.  Regression: the queue pass
+one batched launch, and repeated runs agree; so does the dense pass (the
+f16-split x . C^T of every fit on the matrix cores, exact recheck of near
+ties), every iteration or until fewer than 9 fits run (then bounded passes
+from recomputed bounds); at F = 30 (FMAX = 32) and at
+F = 50 / 45 (FMAX = 64: F-sized LDS tiles, masked tile stores with a zeroed
+pad, the kList gather into the smaller tile; odd F takes the scalar gather).
+The k-means++ passes at F > 32 (F-sized tiles, pipelined table loads) pick
+the oracle's indices on the same fp32 rows.  Regression: the queue pass
 gathers only the F floats of each row into LDS, and the scaled-row read
 took the padded pair of the tile's last row from LDS no pass had written
 (NaN * 0 = NaN): a few labels per pass changed from run to run."""
@@ -16,35 +23,44 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _rows():
+def _rows(C=30, size=1536):
     import milwrm_amd as M
     from milwrm_amd import device as D
 
-    raw, mask = D.synth_slide(1536, 1536, 30, seed=20251015, mode="hard")
+    raw, mask = D.synth_slide(size, size, C, seed=20251015, mode="hard")
     im = M.img.from_device(raw, mask)
     with contextlib.redirect_stdout(sys.stderr):
         est, pix = im.calculate_non_zero_mean()
         df = pd.DataFrame({"Img": [im], "batch_names": ["b"], "mean estimators": [est],
                            "pixels": [pix]})
         lab = M.mxif_labeler(df)
-        lab.prep_cluster_data(features=list(range(30)), sigma=2, fract=0.2)
+        lab.prep_cluster_data(features=list(range(C)), sigma=2, fract=0.2)
     return lab._rows
 
 
 @pytest.mark.timeout(300)
-def test_pass_kinds_equal_full_estep(gpu, monkeypatch):
+@pytest.mark.parametrize("C,size", [(30, 1536), (50, 1024), (45, 1024)])
+def test_pass_kinds_equal_full_estep(gpu, monkeypatch, C, size):
     from milwrm_amd import kmeans as KM
 
-    rows = _rows()
+    rows = _rows(C, size)
     ks = list(range(8, 21))
     out = {}
-    for name, qb, qk, nobound in [("full", -1.0, KM.KIND_QUEUE, True), ("tile", -1.0, KM.KIND_QUEUE, False),
-                                  ("queue", 2.0, KM.KIND_QUEUE, False), ("queue_again", 2.0, KM.KIND_QUEUE, False),
-                                  ("list", 2.0, KM.KIND_LIST, False),
-                                  ("list_again", 2.0, KM.KIND_LIST, False),
-                                  ("default", KM.QUEUE_BELOW, KM.QUEUE_KIND, False)]:
+    # (name, queue threshold, few-undecided kind, no bounds, dense pass from how many fits)
+    for name, qb, qk, nobound, dmin in [("full", -1.0, KM.KIND_QUEUE, True, None),
+                                        ("tile", -1.0, KM.KIND_QUEUE, False, None),
+                                        ("queue", 2.0, KM.KIND_QUEUE, False, None),
+                                        ("queue_again", 2.0, KM.KIND_QUEUE, False, None),
+                                        ("list", 2.0, KM.KIND_LIST, False, None),
+                                        ("list_again", 2.0, KM.KIND_LIST, False, None),
+                                        ("dense", 2.0, KM.KIND_LIST, False, 1),
+                                        ("dense_again", 2.0, KM.KIND_LIST, False, 1),
+                                        ("dense_then_bounds", KM.QUEUE_BELOW, KM.QUEUE_KIND, False, 9),
+                                        ("default", KM.QUEUE_BELOW, KM.QUEUE_KIND, False, KM.DENSE_MIN_FITS)]:
         monkeypatch.setattr(KM, "QUEUE_BELOW", qb)
         monkeypatch.setattr(KM, "QUEUE_KIND", qk)
+        monkeypatch.setattr(KM, "USE_DENSE", dmin is not None)
+        monkeypatch.setattr(KM, "DENSE_MIN_FITS", dmin or 1)
         if nobound:
             monkeypatch.setenv("MW_LLOYD_NOBOUND", "1")
         else:
@@ -52,9 +68,31 @@ def test_pass_kinds_equal_full_estep(gpu, monkeypatch):
         with contextlib.redirect_stdout(sys.stderr):
             fits = KM.fit_many(rows, ks, random_state=18)
         out[name] = [(np.asarray(m.labels_).copy(), m.cluster_centers_.copy(), m.n_iter_) for m in fits]
-    for name in ("tile", "queue", "queue_again", "list", "list_again", "default"):
+    for name in ("tile", "queue", "queue_again", "list", "list_again", "dense", "dense_again",
+                 "dense_then_bounds", "default"):
         for i, k in enumerate(ks):
             a, b = out["full"][i], out[name][i]
             assert a[2] == b[2], f"k={k} {name}: n_iter {b[2]} vs {a[2]}"
             np.testing.assert_array_equal(b[0], a[0], err_msg=f"k={k} {name} labels")
             np.testing.assert_array_equal(b[1], a[1], err_msg=f"k={k} {name} centers")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("C", [50, 45])
+def test_kpp_indices_wide_rows(gpu, C):
+    """k-means++ at F > 32 (FMAX = 64 instances) against the oracle's
+    _kmeans_plusplus restatement on the same fp32 rows (scaled, centered as
+    KMeans.fit does), k = 8 and 20."""
+    import torch
+
+    from milwrm_amd.kmeans import KMeans
+    from oracle import milwrm_oracle as O
+
+    rows = _rows(C, 768)
+    Xs = ((rows.X.double() - torch.from_numpy(rows.mu).cuda()) * torch.from_numpy(rows.inv).cuda()).cpu().numpy()
+    Xs -= Xs.mean(axis=0)
+    for k in (8, 20):
+        with contextlib.redirect_stdout(sys.stderr):
+            km = KMeans(n_clusters=k, random_state=18).fit(rows)
+        _, idx = O.kmeans_plusplus(Xs, k, np.random.RandomState(18))
+        np.testing.assert_array_equal(km.init_indices_, idx, err_msg=f"F={C} k={k}")

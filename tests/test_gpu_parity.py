@@ -608,3 +608,48 @@ def test_st_labeler_k8(gpu, golden):
         np.testing.assert_allclose(ads[s].obs["confidence_score"].values, g8[f"conf{s}"], rtol=RTOL,
                                    atol=RTOL)
     np.testing.assert_allclose(lab.confidence_score_df.values, g8["confidence_score_df"], rtol=RTOL)
+
+
+@pytest.mark.parametrize("n,density", [(64, 1.0), (65, 0.5), (4097, 0.85), (100_003, 0.01), (262_144, 1.0),
+                                       (1_000_000, 0.85)])
+def test_rank_index_gather_equals_table(gpu, n, density):
+    """The compact rank index (mw_mask_rank_index: per 64-pixel word its mask
+    bits and prefix, per 64 ranks a word) maps every draw to the pixel the
+    rank -> pixel table gives: rows, column statistics and the sample slots
+    bitwise equal; partial last words, empty words, M a multiple of 64."""
+    import torch
+
+    from milwrm_amd import _native as N
+    from milwrm_amd import device as D
+    from milwrm_amd.rng import subsample_indices_device
+
+    rs = np.random.RandomState(n)
+    C = 6
+    mask = (rs.random_sample(n) < density).astype(np.uint8)
+    if n == 4097:
+        mask[128:640] = 0  # whole empty words
+    img = torch.from_numpy(rs.random_sample((n, 1, C)).astype(np.float32)).cuda()
+    m = D.padded_mask(torch.from_numpy(mask).cuda())
+    M = int(mask.sum())
+    cnt = torch.empty(1, dtype=torch.int64, device="cuda")
+    ws = D.WS.get("mrank", N.query("mw_mask_rank_ws_bytes", n))
+    r2p = torch.empty(n, dtype=torch.int32, device="cuda")
+    N.call("mw_mask_rank", D.P(m), n, D.P(r2p), D.P(cnt), D.P(ws), D.stream())
+    assert int(cnt.item()) == M
+    ix = torch.empty(N.query("mw_rank_index_bytes", n), dtype=torch.uint8, device="cuda")
+    N.call("mw_mask_rank_index", D.P(m), n, D.P(ix), D.P(cnt), D.P(ws), D.stream())
+    assert int(cnt.item()) == M
+    ri = D.RankIndex(ix, n)
+    np.random.seed(16)
+    idx, _ = subsample_indices_device(M, 0.9, 16, torch.device("cuda"))
+    S = int(idx.shape[0])
+    feat = torch.arange(C, dtype=torch.int32, device="cuda")
+    out = []
+    for table in (r2p, ri):
+        X = torch.empty((S, C), dtype=torch.float32, device="cuda")
+        st = torch.zeros(1 + 2 * C, dtype=torch.float64, device="cuda")
+        D.gather_rows(img, feat, idx, table, X, st, accumulate=False)
+        out.append((X.cpu().numpy(), st.cpu().numpy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    np.testing.assert_array_equal(out[1][0], img.reshape(n, C).cpu().numpy()[np.nonzero(mask)[0][idx.cpu().numpy()]])

@@ -318,3 +318,28 @@ def test_use_paths_npz_round_trip(gpu, golden, tmp_path):
         np.testing.assert_array_equal(np.nan_to_num(lab.tissue_IDs[i], nan=-1),
                                       np.nan_to_num(mem.tissue_IDs[i], nan=-1))
     np.testing.assert_array_equal(lab.confidence_score_df.values, mem.confidence_score_df.values)
+
+
+def test_qc_nonfinite_feature_gives_nan(gpu):
+    """A non-finite value in a slide (fp32 input) has no fixed point in the
+    exact QC sums: the quantities of its feature are NaN, as the reference's
+    numpy sums are; the other features keep their values."""
+    from milwrm_amd import MILWRM as MW
+    import milwrm_amd as M
+
+    raw, mask = O.synth_slide(64, 80, 4, seed=5, mode="hard")
+    x = raw.astype(np.float32)
+    tid = np.where(mask != 0, (np.arange(64 * 80).reshape(64, 80) % 3).astype(np.float64), np.nan)
+    cents = np.random.RandomState(0).normal(size=(3, 4))
+    sc = _scaler(np.zeros(4), np.full(4, 100.0))
+    clean = MW.estimate_mse_mxif([M.img(x.copy(), mask=mask.copy())], False, [tid], sc, cents,
+                                 list(range(4)), 3)
+    x[10, 20, 2] = np.nan
+    im = M.img(x, mask=mask.copy())
+    pv = MW.estimate_percentage_variance_mxif(im, False, sc, cents, list(range(4)), tid)
+    assert np.isnan(pv)
+    mse = MW.estimate_mse_mxif([M.img(x.copy(), mask=mask.copy())], False, [tid], sc, cents,
+                               list(range(4)), 3)
+    for d in range(3):
+        assert np.isnan(mse[d][0][2])
+        np.testing.assert_array_equal(np.delete(mse[d][0], 2), np.delete(clean[d][0], 2))

@@ -80,15 +80,20 @@ def _assert_same(a, b):
         np.testing.assert_array_equal(a["mse"], b["mse"])
 
 
-@pytest.mark.parametrize("C,dtype,band", [(8, np.uint16, "37"), (50, np.uint16, "61"), (7, np.uint16, "29"),
-                                          (8, np.uint8, "200")])
-def test_streamed_equals_resident(gpu, monkeypatch, C, dtype, band):
+@pytest.mark.parametrize("C,dtype,band,rank", [(8, np.uint16, "37", "table"), (8, np.uint16, "37", "index"),
+                                               (50, np.uint16, "61", "index"), (7, np.uint16, "29", "table"),
+                                               (8, np.uint8, "200", "index")])
+def test_streamed_equals_resident(gpu, monkeypatch, C, dtype, band, rank):
+    """Streamed == resident, bitwise; the streamed run draws through the rank
+    table or the compact rank index (the resident one through the table)."""
     from milwrm_amd import device as D
 
     slides = _slides(C, dtype=dtype)
     monkeypatch.delenv("MW_HBM_BUDGET", raising=False)
+    monkeypatch.setattr(D, "RANK_TABLE_MAX_PIX", 1 << 62)
     ref = _pipeline(slides)
     assert all(ref["resident"])
+    monkeypatch.setattr(D, "RANK_TABLE_MAX_PIX", 1 << 62 if rank == "table" else 0)
     monkeypatch.setenv("MW_HBM_BUDGET", "1")       # nothing may stay resident: every pass streams
     monkeypatch.setenv("MW_STREAM_BAND_ROWS", band)
     before = dict(D.FUSED_USED)
