@@ -258,7 +258,8 @@ int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu,
  *   drift     k fp32 |c_j - c_j(previous pass)|, rounded up (0 on the first pass)
  *   half_sep  k fp32 0.5 * min_{i != j} |c_i - c_j|, rounded down (+inf for k = 1)
  *   drift_max max_j drift[j]
- *   ws        mw_lloyd_ws_bytes(S, k, F) bytes of per-block records
+ *   ws        mw_lloyd_ws_bytes(S, k, F) bytes of per-block records and row lists
+ *             (mw_lloyd_ws_bytes_kinds(S, k, F, 0): records only, no kind 4)
  *   out       mw_lloyd_rec_len(k, F) fp64, the fixed-order fold of the records:
  *             [dQ_hi k*F | dQ_lo k*F | dcount k | changed | recomputed | in_hi | in_lo]
  * mode 0: E-step (rows whose bounds prove the label skip the distances) and
@@ -293,6 +294,10 @@ typedef struct mw_lloyd_fit {
 } mw_lloyd_fit;
 int mw_lloyd_rec_len(int k, int F);
 size_t mw_lloyd_ws_bytes(int64_t S, int k, int F);
+/* The workspace without the kList row lists (4 bytes per row) when with_list
+ * is 0 or S >= 2^31 (kind 4 falls back to kind 2 there): a fit whose passes
+ * never take kind 4 (MW_LLOYD_LIST=0) needs only its per-block records. */
+size_t mw_lloyd_ws_bytes_kinds(int64_t S, int k, int F, int with_list);
 int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
                   const int32_t* d_qexp, int n, const mw_lloyd_fit* h_fits, int mode, int kind,
                   void* stream);

@@ -60,6 +60,7 @@ _PROTOS = {
     "mw_kpp_search": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "mw_kpp_trial": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_lloyd_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
+    "mw_lloyd_ws_bytes_kinds": (c_sz, [c_i64, c_i32, c_i32, c_i32]),
     "mw_lloyd_rec_len": (c_i32, [c_i32, c_i32]),
     "mw_lloyd_pass": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "mw_col_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),

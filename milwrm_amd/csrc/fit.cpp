@@ -328,6 +328,13 @@ struct FitLayout {
   size_t small, par, ub, lb, lws, out, big, total;
 };
 static inline size_t fal(size_t x) { return (x + 255) & ~(size_t)255; }
+static int lloyd_queue_kind() {  // MW_LLOYD_LIST=0: one-kernel kQueue (A/B)
+  static const int q = [] {
+    const char* e = getenv("MW_LLOYD_LIST");
+    return (e && e[0] == '0') ? 2 : 4;  // as kmeans.QUEUE_KIND
+  }();
+  return q;
+}
 static FitLayout fit_layout(int64_t S, int F, int k) {
   const int T = 2 + (int)std::log((double)(k < 1 ? 1 : k));
   FitLayout L;
@@ -336,7 +343,7 @@ static FitLayout fit_layout(int64_t S, int F, int k) {
   L.ub = L.par + fal(((size_t)k * F + 2 * k) * 4);
   L.lb = L.ub + fal((size_t)S * 4);
   L.lws = L.lb + fal((size_t)S * 4);
-  L.out = L.lws + fal(mw_lloyd_ws_bytes(S, k, F));
+  L.out = L.lws + fal(mw_lloyd_ws_bytes_kinds(S, k, F, lloyd_queue_kind() == 4));
   L.big = L.out + fal((size_t)mw_lloyd_rec_len(k, F) * 8);
   size_t big = mw_gather_ws_bytes(S, F);
   if (T <= 8) big = std::max(big, mw_kpp_ws_bytes(S, T));
@@ -520,10 +527,7 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
       const char* e = getenv("MW_LLOYD_QUEUE_BELOW");
       return e ? atof(e) : 0.3;  // as kmeans.QUEUE_BELOW
     }();
-    static const int queue_kind = [] {  // MW_LLOYD_LIST=0: one-kernel kQueue (A/B)
-      const char* e = getenv("MW_LLOYD_LIST");
-      return (e && e[0] == '0') ? 2 : 4;  // as kmeans.QUEUE_KIND
-    }();
+    const int queue_kind = lloyd_queue_kind();
     int kind = first_kind;  // first pass
     if (last_recomputed >= 0) {
       double frac = (double)last_recomputed / (double)S;

@@ -116,6 +116,7 @@ constexpr int kTile = 1;   // stream every tile's rows; bounds skip the E-step p
 constexpr int kQueue = 2;  // stream only the row state; read the undecided rows
 constexpr int kFirstAtomic = 3;  // kFirst with the sums by LDS atomics (A/B)
 constexpr int kList = 4;  // kQueue as two launches: lloyd_mark_kernel lists, this kernel reads
+constexpr int kFirstSum = 7;  // kFirst with per-feature fp64 sums of label-sorted rows (internal, k <= 16)
 
 // One pass of fit g = blockIdx.x % n over row block blockIdx.x / n (the n
 // blocks that read one row block are dispatched together: rows that several
@@ -469,6 +470,13 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
     constexpr int MBX = MBT * NB;
     constexpr int MB = MBT;
     constexpr bool mfma_m = MODE == 0 && KIND == kFirst;
+    // kFirstSum: lane = feature, one fp64 sum per label of the q of the
+    // label's rows (integers below 2^41: exact; flushed every 32 tiles)
+    constexpr int KS = (MODE == 0 && KIND == kFirstSum) ? 16 : 1;
+    double fsum[KS];
+#pragma unroll
+    for (int j = 0; j < KS; ++j) fsum[j] = 0.0;
+    const int fe = lane < F ? s_e[lane] : 0;
     static_assert(KIND != kFirstAtomic || MODE == 0, "atomic first pass is mode 0");
     typedef double d4v __attribute__((ext_vector_type(4)));
     d4v acc[mfma_m ? MBX : 1];
@@ -489,6 +497,14 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
             }
           }
           acc[i] = d4v{0.0, 0.0, 0.0, 0.0};
+        }
+      }
+      if constexpr (MODE == 0 && KIND == kFirstSum) {
+#pragma unroll
+        for (int j = 0; j < KS; ++j) {
+          if (j < k && lane < F && fsum[j] != 0.0)
+            atomicAdd(&s_acc[j * F + lane], (unsigned long long)(long long)fsum[j]);
+          fsum[j] = 0.0;
         }
       }
     };
@@ -571,6 +587,36 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
           move_rows(__ballot(ch), lab, 255);
           continue;
         }
+        if constexpr (MODE == 0 && KIND == kFirstSum) {
+          // per label: its rows by their ballot bits (scalar bit scans), 4
+          // LDS reads in flight, lane = feature
+          const float* xcol = s_tile + (lane < F ? lane : 0);
+#pragma unroll
+          for (int j = 0; j < KS; ++j) {
+            if (j >= k) break;  // wave-uniform
+            unsigned long long m = __ballot(valid && lab == j);
+            if (lane == 0 && m) atomicAdd(&s_cnt[j], __popcll(m));
+            double sj = 0.0;
+            while (m != 0ull) {  // wave-uniform
+              int r[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                r[u] = m != 0ull ? __builtin_ctzll(m) : -1;
+                m &= m - 1ull;
+              }
+              float xv[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) xv[u] = r[u] >= 0 ? xcol[r[u] * F] : 0.f;
+#pragma unroll
+              for (int u = 0; u < 4; ++u) sj += rint(ldexp((double)xv[u], fe));
+            }
+            fsum[j] += sj;
+          }
+          if (++since_flush == 32) {  // sums stay below 32 * 64 * 2^41 = 2^52: exact
+            flush();
+            since_flush = 0;
+          }
+        }
         if constexpr (MODE == 0 && KIND == kFirst) {
           if (valid) atomicAdd(&s_cnt[lab], 1);
           s_lab[lane] = valid ? lab : -1;
@@ -642,12 +688,13 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
 // 256 VGPRs and an 8-byte spill).  Config-5 cohort fit (2 x 40k^2 x 50
 // slides, same box, profiles/r04/bench_c5x2_synth*.json): 476.3 -> 460.4 ms.
 // The default; MW_LLOYD_FIRST_W2=0 takes the unbounded instance (same bits)
+template <int KIND>
 __global__ void __launch_bounds__(256, 2) lloyd_first_w2_kernel(const float* __restrict__ X, int64_t S, int F,
                                                                const float* __restrict__ ga,
                                                                const float* __restrict__ gb,
                                                                const int* __restrict__ qexp,
                                                                const LloydFitsArg fits, int n, int64_t R) {
-  lloyd_pass_body<64, 0, kFirst, 1>(X, S, F, ga, gb, qexp, fits, n, R);
+  lloyd_pass_body<64, 0, KIND, 1>(X, S, F, ga, gb, qexp, fits, n, R);
 }
 
 // kList, first launch: the bound test of every row of the block's range from
@@ -806,6 +853,11 @@ size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
   return lloyd_list_off(G, k, F) + lloyd_al256((size_t)G * 4) + (size_t)G * krows(S) * 4 + 256;
 }
 
+size_t mw_lloyd_ws_bytes_kinds(int64_t S, int k, int F, int with_list) {
+  if (with_list && S < ((int64_t)1 << 31)) return mw_lloyd_ws_bytes(S, k, F);
+  return lloyd_list_off(kblocks(S), k, F) + 256;  // records only: kind 4 is never passed
+}
+
 int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream) {
   MW_CHECK_ARG(d_X && d_out && S > 0 && F > 0 && F <= kColAbsMaxF, "mw_col_absmax: bad arguments (F <= %d)",
                kColAbsMaxF);
@@ -902,6 +954,11 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   // blocks, at most 4 (else the sums go through LDS atomics)
   const int NBF = FM <= 16 ? 1 : FM / 16, MBF = (kmax + 15) / 16;
   if (mode == 0 && kind == kFirst && MBF * NBF > 4) kind = kFirstAtomic;
+  static const bool first_sum = [] {
+    const char* e = getenv("MW_LLOYD_FIRST_SUM");
+    return e && e[0] == '1';
+  }();
+  if (first_sum && mode == 0 && kind == kFirst && kmax <= 16) kind = kFirstSum;
   if (mode == 0 && kind == kList) {
     hipLaunchKernelGGL(lloyd_mark_kernel, grid, dim3(256), 0, s, fits, n, S, F, R);
     MW_LAUNCH_CHECK();
@@ -918,6 +975,7 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     }                                                                            \
     else if (kind == kTile) MW_LP(FMV, 0, kTile, 1);                            \
     else if (kind == kFirstAtomic) MW_LP(FMV, 0, kFirstAtomic, 1);              \
+    else if (kind == kFirstSum) MW_LP(FMV, 0, kFirstSum, 1);                    \
     else if (kind == kList) MW_LP(FMV, 0, kList, 1);                            \
     else MW_LP(FMV, 0, kQueue, 1);                                              \
   } else if (mode == 1) MW_LP(FMV, 1, kFirst, 1);                               \
@@ -926,8 +984,12 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     const char* e = getenv("MW_LLOYD_FIRST_W2");
     return !(e && e[0] == '0');
   }();
-  if (first_w2 && FM == 64 && mode == 0 && kind == kFirst && MBF == 1) {
-    hipLaunchKernelGGL(lloyd_first_w2_kernel, grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp, fits, n, R);
+  if (first_w2 && FM == 64 && mode == 0 && (kind == kFirst || kind == kFirstSum) && MBF == 1) {
+    if (kind == kFirst)
+      hipLaunchKernelGGL(lloyd_first_w2_kernel<kFirst>, grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp, fits, n, R);
+    else
+      hipLaunchKernelGGL(lloyd_first_w2_kernel<kFirstSum>, grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp, fits, n,
+                         R);
   } else if (FM == 8) { MW_LPF(8) }
   else if (FM == 16) { MW_LPF(16) }
   else if (FM == 32) { MW_LPF(32) }

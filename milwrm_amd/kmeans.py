@@ -282,7 +282,7 @@ def _check_fit_memory(rows: DeviceRows, ks) -> None:
     S, F = rows.S, rows.F
     from .stream import RESIDENCY
 
-    need = sum(S * 9 + N.query("mw_lloyd_ws_bytes", S, k, F) for k in ks)
+    need = sum(S * 9 + lloyd_ws_bytes(S, k, F) for k in ks)
     free = RESIDENCY.release(need)  # resident copies of host-backed slides go first (stream.py)
     if need > free:
         raise MemoryError(
@@ -307,7 +307,7 @@ class _FitState:
         self.labels = torch.full((S,), 255, dtype=torch.uint8, device=dev)  # 255 = no label yet
         self.ub = torch.empty(S, dtype=torch.float32, device=dev)
         self.lb = torch.empty(S, dtype=torch.float32, device=dev)
-        self.ws = torch.empty(N.query("mw_lloyd_ws_bytes", S, k, F), dtype=torch.uint8, device=dev)
+        self.ws = torch.empty(lloyd_ws_bytes(S, k, F), dtype=torch.uint8, device=dev)
         self.done = False
         self.strict = False
         self.n_iter = 0
@@ -349,6 +349,12 @@ USE_DENSE = os.environ.get("MW_LLOYD_DENSE", "1") != "0"
 # rows in a second) unless MW_LLOYD_LIST=0 (kQueue: both phases chunk by chunk
 # in one kernel)
 QUEUE_KIND = KIND_QUEUE if os.environ.get("MW_LLOYD_LIST") == "0" else KIND_LIST
+
+
+def lloyd_ws_bytes(S: int, k: int, F: int) -> int:
+    """A fit's pass workspace: the per-block records, plus the kList row lists
+    (4 bytes per row) only when the passes can take kList."""
+    return N.query("mw_lloyd_ws_bytes_kinds", S, k, F, int(QUEUE_KIND == KIND_LIST))
 # a mode-0 pass streams every row (kTile) while the previous pass recomputed
 # more than this fraction of the rows, else only the undecided ones (kQueue):
 # the k = 2..20 sweep at 10k^2 x 30 (tools/sweep_bench.py) took 0.77 / 0.69 s

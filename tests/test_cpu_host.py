@@ -156,6 +156,11 @@ def test_lloyd_workspace_holds_records_and_row_lists():
         ws = N.query("mw_lloyd_ws_bytes", S, k, F)
         rec = N.query("mw_lloyd_rec_len", k, F) * 8
         assert ws >= rec + 4 * S, (S, k, F, ws)
+        # without kList: the records only (MW_LLOYD_LIST=0, or S >= 2^31)
+        ws0 = N.query("mw_lloyd_ws_bytes_kinds", S, k, F, 0)
+        assert rec <= ws0 and ws - ws0 >= 4 * S, (S, k, F, ws0)
+        assert N.query("mw_lloyd_ws_bytes_kinds", S, k, F, 1) == ws
+    assert N.query("mw_lloyd_ws_bytes_kinds", 1 << 31, 8, 30, 1) == N.query("mw_lloyd_ws_bytes_kinds", 1 << 31, 8, 30, 0)
 
 
 def test_stream_band_plan_covers_rows():
