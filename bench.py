@@ -61,7 +61,9 @@ def parse():
     ap.add_argument("--size", type=int, default=10000, help="slide is size x size pixels")
     ap.add_argument("--channels", type=int, default=30)
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--mode", default="hard", choices=["hard", "easy"])
+    ap.add_argument("--mode", default="hard", choices=["hard", "easy", "design"],
+                    help="synthetic slide: hard (the headline), design (overlapping domains: "
+                         "SURVEY 8d's I~17 Lloyd iterations), easy")
     ap.add_argument("--slides-per-gpu", type=int, default=1,
                     help="slides each rank labels per step (config 5: 2 on 8 GPUs)")
     ap.add_argument("--source", default="auto", choices=["auto", "device", "synth", "host"],

@@ -107,6 +107,7 @@ __host__ __device__ inline size_t lloyd_lds_bytes(int FMAX, int k, int F, int mo
   if (mode == 0) b += ((size_t)k * F * 8 + 15) & ~(size_t)15;
   b += 4 * (lloyd_tile_bytes(FMAX, F) + 64 * 4);
   if (mode == 0 && kind == 2) b += (size_t)kChunk * 2;  // kQueue
+  if (mode == 0 && kind == 4) b += 4 * 128 * 4;  // kList: per-wave full E-step queues
   return b;
 }
 
@@ -269,6 +270,92 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
     move_rows(__ballot(ch), lab, lab_old);
   };
 
+  // ---- rows that need every distance (kList): a per-wave queue of
+  // row indices, finished 64 at a time with every lane busy ----
+  int* s_q2 = reinterpret_cast<int*>(s_q) + wid * 128;  // (per wave; kList LDS only)
+  // the rows s_idx[0 .. cnt_b) into the wave tile (row j at s_tile + j*F)
+  auto gather = [&](const int* s_idx, int cnt_b) {
+    if ((F & 1) == 0) {
+      const int P2 = F >> 1;
+      int j = lane / P2, c = lane - (lane / P2) * P2;  // piece (j, c) = p, stepped by 64
+      const int dj = 64 / P2, dc = 64 - dj * P2;
+      constexpr int kGB = 8;
+      for (int i0 = 0; i0 < P2; i0 += kGB) {
+        f2v v[kGB];
+        int dst[kGB];
+#pragma unroll
+        for (int i = 0; i < kGB; ++i) {
+          const bool ok = i0 + i < P2;
+          const int64_t rj = s_idx[j < cnt_b ? j : 0];
+          v[i] = ok ? *reinterpret_cast<const f2v*>(X + rj * F + 2 * c) : f2v{0.f, 0.f};
+          dst[i] = ok ? j * F + 2 * c : -1;
+          j += dj;
+          c += dc;
+          if (c >= P2) { c -= P2; ++j; }
+        }
+#pragma unroll
+        for (int i = 0; i < kGB; ++i)
+          if (dst[i] >= 0) *reinterpret_cast<f2v*>(s_tile + dst[i]) = v[i];
+      }
+    } else {
+      for (int p = lane; p < 64 * F; p += 64) {
+        const int j = p / F, c = p - j * F;
+        const int64_t rj = s_idx[j < cnt_b ? j : 0];
+        s_tile[j * F + c] = X[rj * F + c];
+      }
+    }
+  };
+  // stage B over s_q2[0 .. cnt_b)
+  auto full_rows = [&](int cnt_b) {
+    const bool valid = lane < cnt_b;
+    const int64_t r = s_q2[valid ? lane : 0];
+    const int lab_old = labels[r];
+    gather(s_q2, cnt_b);
+    f2v x2[FMAX / 2];
+    load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
+    int ln;
+    float m1, m2;
+    nearest_centers<FMAX, 64, true>(x2, s_cT, k, ln, m1, m2);
+    const bool ch = valid && ln != lab_old;
+    recomputed += valid ? 1 : 0;
+    changed += ch ? 1 : 0;
+    if (valid) {
+      if (ch) labels[r] = (uint8_t)ln;
+      ubuf[r] = sqrtf(m1);
+      lbuf[r] = k > 1 ? sqrtf(m2) : __builtin_inff();
+    }
+    move_rows(__ballot(ch), ln, lab_old);
+    __builtin_amdgcn_wave_barrier();  // s_tile is rewritten next
+  };
+  int nq2 = 0;  // queued rows (wave-uniform)
+  // stage A of a lane's undecided row r (tile rows in s_tile): the own-center
+  // distance tightens ub; decided rows are stored, the rest queued
+  auto tighten_or_queue = [&](bool valid, int64_t r, int lab_old, float ub, float lbv, float thr, auto&& store) {
+    const bool has_old = lab_old < k;
+    const int la = has_old ? lab_old : 0;
+    f2v x2[FMAX / 2];
+    load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
+    if (has_old) ub = sqrtf(dist_one<FMAX>(x2, s_cT, la));
+    const bool need2 = valid && !(has_old && ub * (1.f + kEps) < thr);
+    if (valid && !need2) store(true, false, lab_old, ub, lbv);  // the label stays
+    const unsigned long long m = __ballot(need2);
+    if (need2) s_q2[nq2 + __popcll(m & ((1ull << lane) - 1ull))] = (int)r;
+    nq2 += __popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto drain = [&](bool all) {  // stage B on each full 64 (all: the remainder too)
+    if (nq2 >= 64) {
+      full_rows(64);
+      nq2 -= 64;
+      if (lane < nq2) s_q2[lane] = s_q2[64 + lane];  // carry the rest (< 64) to the front
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (all && nq2 > 0) {
+      full_rows(nq2);
+      nq2 = 0;
+    }
+  };
+
   if constexpr (MODE == 0 && KIND == kQueue) {
     // =========================== queue pass ===========================
     for (int64_t c0 = lo; c0 < hi; c0 += kChunk) {
@@ -397,6 +484,12 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
     }
   } else if constexpr (MODE == 0 && KIND == kList) {
     // ============================ list pass =============================
+    // Two stages per wave: (A) the listed rows, 64 at a time: gather, the
+    // own-center distance tightens the upper bound, rows it decides are done;
+    // the rest go to a per-wave queue of rows that need every distance; (B)
+    // each full 64 of that queue (and the remainder at the end) runs the
+    // k-distance E-step with every lane busy.  The decisions are those of
+    // finish_rows (same tests, same arithmetic): same labels, same sums.
     const int G = (int)(gridDim.x / n);
     const char* wsb = reinterpret_cast<const char*>(fit.ws);
     const size_t loff = lloyd_list_off(G, k, F);
@@ -413,49 +506,18 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
       const float ub_in = ubuf[r], lb_in = lbuf[r];
       s_row[lane] = (int)r;
       __builtin_amdgcn_wave_barrier();
-      if ((F & 1) == 0) {
-        const int P2 = F >> 1;
-        int j = lane / P2, c = lane - (lane / P2) * P2;  // piece (j, c) = p, stepped by 64
-        const int dj = 64 / P2, dc = 64 - dj * P2;
-        constexpr int kGB = 8;
-        for (int i0 = 0; i0 < P2; i0 += kGB) {
-          f2v v[kGB];
-          int dst[kGB];
-#pragma unroll
-          for (int i = 0; i < kGB; ++i) {
-            const bool ok = i0 + i < P2;
-            const int64_t rj = s_row[j < cnt_b ? j : 0];
-            v[i] = ok ? *reinterpret_cast<const f2v*>(X + rj * F + 2 * c) : f2v{0.f, 0.f};
-            dst[i] = ok ? j * F + 2 * c : -1;
-            j += dj;
-            c += dc;
-            if (c >= P2) { c -= P2; ++j; }
-          }
-#pragma unroll
-          for (int i = 0; i < kGB; ++i)
-            if (dst[i] >= 0) *reinterpret_cast<f2v*>(s_tile + dst[i]) = v[i];
-        }
-      } else {
-        for (int p = lane; p < 64 * F; p += 64) {
-          const int j = p / F, c = p - j * F;
-          const int64_t rj = s_row[j < cnt_b ? j : 0];
-          s_tile[j * F + c] = X[rj * F + c];
-        }
-      }
+      gather(s_row, cnt_b);
       const int la = lab_old < k ? lab_old : 0;
       const float ub = ub_in + s_drift[la];
       const float lbv = lb_in - dmax;
       const float thr = fmaxf(lbv, s_half[la]);
-      finish_rows(valid, valid, lab_old, ub, lbv, thr,
-                  [&](bool v, bool ch, int lab, float u, float l) {
-                    if (v) {
-                      if (ch) labels[r] = (uint8_t)lab;
-                      ubuf[r] = u;
-                      lbuf[r] = l;
-                    }
-                  });
-      __builtin_amdgcn_wave_barrier();  // s_row is rewritten by the next batch
+      tighten_or_queue(valid, r, lab_old, ub, lbv, thr, [&](bool, bool, int, float u, float l) {
+        ubuf[r] = u;
+        lbuf[r] = l;
+      });
+      drain(false);
     }
+    drain(true);
   } else {
     // ========================== streamed tiles ==========================
     const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
@@ -948,7 +1010,6 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     return MW_OK;
   }
   const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
-  const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
   const dim3 grid((unsigned)G * (unsigned)n);
   // kFirst: fp64 accumulators for ceil(kmax / 16) label blocks x the feature
   // blocks, at most 4 (else the sums go through LDS atomics)
@@ -959,6 +1020,7 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     return e && e[0] == '1';
   }();
   if (first_sum && mode == 0 && kind == kFirst && kmax <= 16) kind = kFirstSum;
+  const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
   if (mode == 0 && kind == kList) {
     hipLaunchKernelGGL(lloyd_mark_kernel, grid, dim3(256), 0, s, fits, n, S, F, R);
     MW_LAUNCH_CHECK();

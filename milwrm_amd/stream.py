@@ -272,9 +272,22 @@ def pinned_rows(src: RowSource, chunk_bytes: int = 1 << 30, progress=None) -> li
     return out
 
 
+# generator modes: (lognormal spread of the domain profiles, gamma shape of
+# the noise); "design" overlaps the domains so that the k = 8 fit runs near
+# SURVEY 8d's I = 17 Lloyd iterations (MW_SYNTH_SPREAD overrides its spread)
+SYNTH_MODES = {"hard": (0.15, 1), "easy": (0.8, 4), "design": (0.05, 1)}
+
+
+def synth_mode(mode):
+    sp_, shape = SYNTH_MODES[mode]
+    if mode == "design" and os.environ.get("MW_SYNTH_SPREAD"):
+        sp_ = float(os.environ["MW_SYNTH_SPREAD"])
+    return sp_, shape
+
+
 def _synth_params(H, W, C, seed, mode="hard", n_seeds=32, n_domains=8, bg_frac=0.15):
     rng = np.random.default_rng(seed)
-    sp_, shape = (0.15, 1) if mode == "hard" else (0.8, 4)
+    sp_, shape = synth_mode(mode)
     syx = np.stack([rng.uniform(0, H, n_seeds), rng.uniform(0, W, n_seeds)], 1).astype(np.float32)
     prof = rng.lognormal(4.0, sp_, size=(n_domains, C)).astype(np.float32)
     return syx, prof, shape, int(round(bg_frac * H)), n_seeds, n_domains
