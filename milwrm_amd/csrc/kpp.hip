@@ -143,19 +143,12 @@ __device__ __forceinline__ double kpp_dist_row(const float* __restrict__ x, int 
 // stream and the T + 2 chains: <= 128 VGPRs, 4 waves per SIMD (FMAX = 64:
 // the 16-KB tiles allow 2 waves per SIMD, so the registers may grow instead
 // of spilling).  All LDS is dynamic (16-B aligned).
-__device__ __forceinline__ double readlane64(double v, int l) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
-  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-
 template <int FMAX, int T, int MODE>
 __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
     const float* __restrict__ X, int64_t S, int F, const double* __restrict__ tab,
     const double* __restrict__ tab_prev, const int* __restrict__ best, int best_val,
     double* __restrict__ cur, int64_t R, int64_t NTL, double* __restrict__ bsum_new,
-    double* __restrict__ tsum_new, int vtab) {
+    double* __restrict__ tsum_new) {
   constexpr int NV = FMAX / 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* s_red = reinterpret_cast<double*>(smem);  // [4] block-sum scratch
@@ -190,20 +183,6 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
   const int pb = MODE == 2 ? (best ? *best : best_val) : 0;
   const double* tp = tab_prev + 64 + pb;
   const double tcc = MODE == 2 ? tab_prev[640 + pb] : 0.0;
-  // vtab (FMAX <= 32, even F): the table in VGPRs instead, lane g holding
-  // feature g's entries, broadcast per feature by v_readlane: no scalar loads
-  // (and no lgkmcnt waits) inside the tile loop
-  double v_inv = 0.0, v_mi = 0.0, v_p = 0.0, v_c[T];
-#pragma unroll
-  for (int c = 0; c < T; ++c) v_c[c] = 0.0;
-  if (FMAX <= 32 && vtab) {
-    const int g = lane & 31;
-    v_inv = tb[g];
-    v_mi = tb[576 + g];
-#pragma unroll
-    for (int c = 0; c < T; ++c) v_c[c] = tb[64 + g * 8 + c];
-    if (MODE == 2) v_p = tp[g * 8];
-  }
   f4v v[NV];
   double cur_next = 0.0;
   auto fetch = [&](int tt) {
@@ -271,28 +250,7 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
 #ifndef MW_KPP_SPIPE
 #define MW_KPP_SPIPE 64  // FMAX from which the pipelined form below is used
 #endif
-      if (FMAX <= 32 && vtab) {
-        // keep the broadcasts inside the tile loop (loop-invariant, they
-        // would be hoisted into more SGPRs than a wave has)
-        asm volatile("" : "+v"(v_inv), "+v"(v_mi), "+v"(v_p));
-#pragma unroll
-        for (int c = 0; c < T; ++c) asm volatile("" : "+v"(v_c[c]));
-        auto bc = [&](int f) {
-          TabF r;
-          r.inv = readlane64(v_inv, f);
-          r.mi = readlane64(v_mi, f);
-#pragma unroll
-          for (int c = 0; c < T; ++c) r.c[c] = readlane64(v_c[c], f);
-          r.pend = MODE == 2 ? readlane64(v_p, f) : 0.0;
-          return r;
-        };
-#pragma unroll
-        for (int p = 0; p < (FMAX < 32 ? FMAX : 32) / 2; ++p) {
-          const f2v x2 = *reinterpret_cast<const f2v*>(xr + 2 * p);
-          featt((double)x2.x, bc(2 * p));
-          featt((double)x2.y, bc(2 * p + 1));
-        }
-      } else if constexpr (FMAX >= MW_KPP_SPIPE) {
+      if constexpr (FMAX >= MW_KPP_SPIPE) {
         // the row's feature pairs into registers first (one LDS wait), then
         // per pair: wait for the table loads issued one pair earlier (nothing
         // else is outstanding on the shared LDS/scalar counter), issue the next
@@ -521,14 +479,9 @@ static int kpp_pass_launch(const float* X, int64_t S, int F, const double* mu, c
   double* bs = p.bsum_of(c, T);
   double* tsm = p.tsum_of(c, T);
   const int64_t R = krows(S);
-  static const int vtab_env = [] {
-    const char* e = getenv("MW_KPP_VTAB");
-    return e ? atoi(e) : 0;
-  }();
-  const int vtab = vtab_env && FM <= 32 && (F & 1) == 0;
 #define MW_KP(FMV, TV, MV)                                                                      \
   hipLaunchKernelGGL((kpp_pass_kernel<FMV, TV, MV>), dim3(p.L.G), dim3(256), lds, s, X, S, F, tab, \
-                     tab_prev, best, best_val, p.cur, R, p.L.NTL, bs, tsm, vtab)
+                     tab_prev, best, best_val, p.cur, R, p.L.NTL, bs, tsm)
 #define MW_KPM(FMV, TV) \
   if (mode == 1) MW_KP(FMV, TV, 1); else MW_KP(FMV, TV, 2);
 #define MW_KPT(FMV)                                                                        \

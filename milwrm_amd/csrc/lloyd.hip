@@ -107,7 +107,6 @@ __host__ __device__ inline size_t lloyd_lds_bytes(int FMAX, int k, int F, int mo
   if (mode == 0) b += ((size_t)k * F * 8 + 15) & ~(size_t)15;
   b += 4 * (lloyd_tile_bytes(FMAX, F) + 64 * 4);
   if (mode == 0 && kind == 2) b += (size_t)kChunk * 2;  // kQueue
-  if (mode == 0 && kind == 4) b += 4 * 128 * 4;  // kList: per-wave full E-step queues
   return b;
 }
 
@@ -270,9 +269,6 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
     move_rows(__ballot(ch), lab, lab_old);
   };
 
-  // ---- rows that need every distance (kList): a per-wave queue of
-  // row indices, finished 64 at a time with every lane busy ----
-  int* s_q2 = reinterpret_cast<int*>(s_q) + wid * 128;  // (per wave; kList LDS only)
   // the rows s_idx[0 .. cnt_b) into the wave tile (row j at s_tile + j*F)
   auto gather = [&](const int* s_idx, int cnt_b) {
     if ((F & 1) == 0) {
@@ -303,56 +299,6 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
         const int64_t rj = s_idx[j < cnt_b ? j : 0];
         s_tile[j * F + c] = X[rj * F + c];
       }
-    }
-  };
-  // stage B over s_q2[0 .. cnt_b)
-  auto full_rows = [&](int cnt_b) {
-    const bool valid = lane < cnt_b;
-    const int64_t r = s_q2[valid ? lane : 0];
-    const int lab_old = labels[r];
-    gather(s_q2, cnt_b);
-    f2v x2[FMAX / 2];
-    load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
-    int ln;
-    float m1, m2;
-    nearest_centers<FMAX, 64, true>(x2, s_cT, k, ln, m1, m2);
-    const bool ch = valid && ln != lab_old;
-    recomputed += valid ? 1 : 0;
-    changed += ch ? 1 : 0;
-    if (valid) {
-      if (ch) labels[r] = (uint8_t)ln;
-      ubuf[r] = sqrtf(m1);
-      lbuf[r] = k > 1 ? sqrtf(m2) : __builtin_inff();
-    }
-    move_rows(__ballot(ch), ln, lab_old);
-    __builtin_amdgcn_wave_barrier();  // s_tile is rewritten next
-  };
-  int nq2 = 0;  // queued rows (wave-uniform)
-  // stage A of a lane's undecided row r (tile rows in s_tile): the own-center
-  // distance tightens ub; decided rows are stored, the rest queued
-  auto tighten_or_queue = [&](bool valid, int64_t r, int lab_old, float ub, float lbv, float thr, auto&& store) {
-    const bool has_old = lab_old < k;
-    const int la = has_old ? lab_old : 0;
-    f2v x2[FMAX / 2];
-    load_scaled_row<FMAX>(s_tile, lane, F, s_a, s_b, x2);
-    if (has_old) ub = sqrtf(dist_one<FMAX>(x2, s_cT, la));
-    const bool need2 = valid && !(has_old && ub * (1.f + kEps) < thr);
-    if (valid && !need2) store(true, false, lab_old, ub, lbv);  // the label stays
-    const unsigned long long m = __ballot(need2);
-    if (need2) s_q2[nq2 + __popcll(m & ((1ull << lane) - 1ull))] = (int)r;
-    nq2 += __popcll(m);
-    __builtin_amdgcn_wave_barrier();
-  };
-  auto drain = [&](bool all) {  // stage B on each full 64 (all: the remainder too)
-    if (nq2 >= 64) {
-      full_rows(64);
-      nq2 -= 64;
-      if (lane < nq2) s_q2[lane] = s_q2[64 + lane];  // carry the rest (< 64) to the front
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (all && nq2 > 0) {
-      full_rows(nq2);
-      nq2 = 0;
     }
   };
 
@@ -511,13 +457,16 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
       const float ub = ub_in + s_drift[la];
       const float lbv = lb_in - dmax;
       const float thr = fmaxf(lbv, s_half[la]);
-      tighten_or_queue(valid, r, lab_old, ub, lbv, thr, [&](bool, bool, int, float u, float l) {
-        ubuf[r] = u;
-        lbuf[r] = l;
-      });
-      drain(false);
+      finish_rows(valid, valid, lab_old, ub, lbv, thr,
+                  [&](bool v, bool ch, int lab, float u, float l) {
+                    if (v) {
+                      if (ch) labels[r] = (uint8_t)lab;
+                      ubuf[r] = u;
+                      lbuf[r] = l;
+                    }
+                  });
+      __builtin_amdgcn_wave_barrier();  // s_row is rewritten by the next batch
     }
-    drain(true);
   } else {
     // ========================== streamed tiles ==========================
     const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
@@ -1015,11 +964,15 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   // blocks, at most 4 (else the sums go through LDS atomics)
   const int NBF = FM <= 16 ? 1 : FM / 16, MBF = (kmax + 15) / 16;
   if (mode == 0 && kind == kFirst && MBF * NBF > 4) kind = kFirstAtomic;
-  static const bool first_sum = [] {
+  // kFirstSum at F > 32 (the config-5 fit 164.7 -> 159.4 ms per slide); at
+  // F <= 32 the one-hot MFMA form measured faster (config-2 fit 7.54 vs 7.74
+  // ms).  MW_LLOYD_FIRST_SUM=1 / 0 forces either.
+  static const int first_sum = [] {
     const char* e = getenv("MW_LLOYD_FIRST_SUM");
-    return e && e[0] == '1';
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
-  if (first_sum && mode == 0 && kind == kFirst && kmax <= 16) kind = kFirstSum;
+  if (mode == 0 && kind == kFirst && kmax <= 16 && (first_sum == 1 || (first_sum < 0 && FM == 64)))
+    kind = kFirstSum;
   const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
   if (mode == 0 && kind == kList) {
     hipLaunchKernelGGL(lloyd_mark_kernel, grid, dim3(256), 0, s, fits, n, S, F, R);

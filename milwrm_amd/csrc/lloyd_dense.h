@@ -261,20 +261,21 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 1 : 2) lloyd_dense_kernel(co
           const int o = dg.off[gi];
           k = fits.f[dg.g0 + gi].k;
           // the fit's (<= 20, 4-aligned) distances in one batch of 16-byte reads
+          // (branch-free: slots past k read as +inf, which changes nothing)
           const f4d* dr = reinterpret_cast<const f4d*>(s_d + nl * kDenseSD + o);
+          const int ulast = (k - 1) >> 2;
           f4d dv[kDenseMaxFitK / 4];
 #pragma unroll
-          for (int u = 0; u < kDenseMaxFitK / 4; ++u)
-            if (4 * u < k) dv[u] = dr[u];
+          for (int u = 0; u < kDenseMaxFitK / 4; ++u) dv[u] = dr[u < ulast ? u : ulast];
           float m1 = dv[0][0], m2 = __builtin_inff();
           lab = 0;
 #pragma unroll
           for (int j = 1; j < kDenseMaxFitK; ++j) {
-            if (j < k) {
-              const float v = dv[j >> 2][j & 3];
-              if (v < m1) { m2 = m1; m1 = v; lab = j; }
-              else if (v < m2) { m2 = v; }
-            }
+            const float v = j < k ? dv[j >> 2][j & 3] : __builtin_inff();
+            const bool lt1 = v < m1, lt2 = v < m2;
+            m2 = lt1 ? m1 : (lt2 ? v : m2);
+            m1 = lt1 ? v : m1;
+            lab = lt1 ? j : lab;
           }
           const float B = bscale * (xx + s_cmax[gi]);
           if (valid && k > 1 && !(m2 - m1 > B)) {

@@ -341,10 +341,12 @@ class _FitState:
 KIND_FIRST, KIND_TILE, KIND_QUEUE, KIND_LIST, KIND_DENSE = 0, 1, 2, 4, 5
 # the batched sweep's dense pass (lloyd_dense.h: x . C^T of every fit in the
 # launch on the matrix cores, exact fp32 recheck of near ties) while at least
-# this many fits run together; fewer -> the bounded passes (MW_LLOYD_DENSE=0:
-# never)
+# this many fits run together; fewer -> the bounded passes.  Opt-in
+# (MW_LLOYD_DENSE=1): the k = 2..20 sweep at config 2 measured 0.91 s with it
+# against 0.70 s with the bounded passes (4.8 ms per dense launch over all
+# fits vs 2.6-2.9 ms per list launch)
 DENSE_MIN_FITS = int(os.environ.get("MW_LLOYD_DENSE_MIN", "3"))
-USE_DENSE = os.environ.get("MW_LLOYD_DENSE", "1") != "0"
+USE_DENSE = os.environ.get("MW_LLOYD_DENSE", "0") == "1"
 # the few-undecided pass: kList (bound test and list in one launch, the listed
 # rows in a second) unless MW_LLOYD_LIST=0 (kQueue: both phases chunk by chunk
 # in one kernel)
