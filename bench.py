@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--size", type=int, default=10000, help="slide is size x size pixels")
     ap.add_argument("--channels", type=int, default=30)
     ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--no-design-point", action="store_true",
+                    help="skip the second line on the design-point slide (--mode design, I~17)")
     ap.add_argument("--mode", default="hard", choices=["hard", "easy", "design"],
                     help="synthetic slide: hard (the headline), design (overlapping domains: "
                          "SURVEY 8d's I~17 Lloyd iterations), easy")
@@ -273,6 +275,37 @@ def check_devices(world: int) -> None:
         sys.exit(2)
 
 
+def design_point(H, W, C, k, comm, lab_hard, steps=3):
+    """The same step on the 'design' slide (overlapping domains: SURVEY 8d's
+    I ~ 17 Lloyd iterations instead of the headline slide's ~5), timed the
+    same way: a second line beside the headline, where the fit weighs as the
+    survey's design point assumes."""
+    from milwrm_amd import profiling
+    from milwrm_amd import stream
+
+    del lab_hard
+    slides = Slides(H, W, C, [20251015], "device", "design")
+    step = make_step(slides, C, k, comm)
+    step()
+    torch.cuda.synchronize()
+    profiling.reset()
+    profiling.enable(True)
+    t0 = time.perf_counter()
+    lab = None
+    for _ in range(steps):
+        lab = None
+        lab = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    profiling.enable(False)
+    prof = profiling.summary()
+    fit = prof.get("kmeans_fit", {})
+    return {"mode": "design", "spread": stream.synth_mode("design")[0], "steps": steps,
+            "ms_per_step": el / steps * 1e3, "value": H * W * steps / el, "unit": "pixels/s",
+            "lloyd_iters": int(lab.kmeans.n_iter_),
+            "kmeans_fit_ms": round(fit.get("total_ms", 0.0) / steps, 4)}
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -428,6 +461,9 @@ def main():
         out["config"]["lloyd_iters"] = n_iter
         out["pipeline_roofline"] = {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,
                                     "unit": "GB/s", "frac": pipe_gbps / (HBM_PEAK_GBPS * world)}
+    if (world == 1 and not args.sweep and args.mode == "hard" and not args.no_design_point
+            and source == "device" and n_sl == 1 and H * W * C * 2 <= 20e9):
+        out["design_point"] = design_point(H, W, C, args.k, comm, lab)
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_size, C, args.k, sweep=args.sweep)
     if rank == 0:

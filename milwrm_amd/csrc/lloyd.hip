@@ -50,8 +50,17 @@ __host__ __device__ inline size_t lloyd_list_off(int G, int k, int F) {
 }
 
 // x as an exact fixed-point integer: rint(x * 2^e) (|x * 2^e| < 2^41; fp64
-// holds it exactly, and sums of up to 2^12 of them)
-__device__ __forceinline__ double fixq64(float x, int e) { return rint(ldexp((double)x, e)); }
+// holds it exactly, and sums of up to 2^12 of them).  Computed in fp32, then
+// widened: x * 2^e is exact in fp32 while it is a normal number (a power-of-two
+// scale of x, and |x * 2^e| < 2^41 cannot overflow); at or above 2^23 it is
+// already an integer, below it rintf's result is an integer < 2^23, so both
+// are exact; below 2^-126 both forms round to zero.  Same value as
+// rint(ldexp((double)x, e)), with one fp64 instruction instead of three.
+__device__ __forceinline__ double fixq64(float x, int e) {
+  float q = rintf(ldexpf(x, e));
+  asm("" : "+v"(q));  // keeps the fp32 ops (hipcc otherwise widens them back to fp64)
+  return (double)q;
+}
 __device__ __forceinline__ long long fixq(float x, int e) { return (long long)fixq64(x, e); }
 
 // int64 -> (hi, lo) integer-valued fp64 limbs
@@ -619,7 +628,7 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
 #pragma unroll
               for (int u = 0; u < 4; ++u) xv[u] = r[u] >= 0 ? xcol[r[u] * F] : 0.f;
 #pragma unroll
-              for (int u = 0; u < 4; ++u) sj += rint(ldexp((double)xv[u], fe));
+              for (int u = 0; u < 4; ++u) sj += fixq64(xv[u], fe);
             }
             fsum[j] += sj;
           }

@@ -275,7 +275,7 @@ def pinned_rows(src: RowSource, chunk_bytes: int = 1 << 30, progress=None) -> li
 # generator modes: (lognormal spread of the domain profiles, gamma shape of
 # the noise); "design" overlaps the domains so that the k = 8 fit runs near
 # SURVEY 8d's I = 17 Lloyd iterations (MW_SYNTH_SPREAD overrides its spread)
-SYNTH_MODES = {"hard": (0.15, 1), "easy": (0.8, 4), "design": (0.05, 1)}
+SYNTH_MODES = {"hard": (0.15, 1), "easy": (0.8, 4), "design": (0.07, 1)}
 
 
 def synth_mode(mode):

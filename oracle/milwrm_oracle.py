@@ -583,7 +583,7 @@ def synth_slide(h, w, c, seed, mode="hard", n_seeds=32, n_domains=8, bg_frac=0.1
     lognormal per-domain channel profiles, gamma noise, top rows background
     (x0.05, mask 0); uint16 HWC + uint8 mask."""
     rng = np.random.default_rng(seed)
-    sp_, shape = {"hard": (0.15, 1.0), "easy": (0.8, 4.0), "design": (0.05, 1.0)}[mode]
+    sp_, shape = {"hard": (0.15, 1.0), "easy": (0.8, 4.0), "design": (0.07, 1.0)}[mode]
     sy = rng.uniform(0, h, n_seeds)
     sx = rng.uniform(0, w, n_seeds)
     dom_of_seed = np.arange(n_seeds) % n_domains
