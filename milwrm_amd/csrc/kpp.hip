@@ -230,21 +230,14 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
       // once per pair (same operations in the same order: same bits; 535 ->
       // 520 us per step pass at config 2, tools/gpu/kvariants.sh)
       struct TabF { double inv, mi, c[T], pend; };
-      // FMAX = 64: the table pointers made opaque per tile: the loads are
-      // loop-invariant, and hoisted out of the tile loop they held every
-      // feature's entries in SGPRs (spilled by the hundred to VGPR lanes, read
-      // back inside the loop)
-      const double* tbt = tb;
-      const double* tpt = tp;
-      if constexpr (FMAX >= 64) asm volatile("" : "+s"(tbt), "+s"(tpt));
       auto ld = [&](int f) {
         TabF r;
         const int g = f < 64 ? f : 63;
-        r.inv = tbt[g];
-        r.mi = tbt[576 + g];
+        r.inv = tb[g];
+        r.mi = tb[576 + g];
 #pragma unroll
-        for (int c = 0; c < T; ++c) r.c[c] = tbt[64 + g * 8 + c];
-        r.pend = MODE == 2 ? tpt[g * 8] : 0.0;
+        for (int c = 0; c < T; ++c) r.c[c] = tb[64 + g * 8 + c];
+        r.pend = MODE == 2 ? tp[g * 8] : 0.0;
         return r;
       };
       auto featt = [&](double xv, const TabF& q) {
@@ -254,14 +247,15 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
 #pragma unroll
         for (int c = 0; c < T; ++c) dot[c] = fma(xs, q.c[c], dot[c]);
       };
-      if constexpr (FMAX >= 64) {
+#ifndef MW_KPP_SPIPE
+#define MW_KPP_SPIPE 64  // FMAX from which the pipelined form below is used
+#endif
+      if constexpr (FMAX >= MW_KPP_SPIPE) {
         // the row's feature pairs into registers first (one LDS wait), then
         // per pair: wait for the table loads issued one pair earlier (nothing
         // else is outstanding on the shared LDS/scalar counter), issue the next
         // pair's table loads, compute from registers only, so the scalar loads
-        // land under the FMAs instead of being waited for with each LDS read.
-        // Scheduling barriers keep each pair's loads in place: left free, hipcc
-        // hoisted loads of many pairs ahead and spilled ~240 SGPRs to VGPR lanes
+        // land under the FMAs instead of being waited for with each LDS read
         f2v xrow[FMAX / 2];
 #pragma unroll
         for (int p = 0; p < FMAX / 2; ++p)
@@ -272,10 +266,8 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
           if (2 * p >= fend) break;  // features past F add exact zeros
           __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): t0, t1 (and the row reads) landed
           const TabF n0 = ld(2 * p + 2), n1 = ld(2 * p + 3);
-          __builtin_amdgcn_sched_barrier(0);
           featt((double)xrow[p].x, t0);
           featt((double)xrow[p].y, t1);
-          __builtin_amdgcn_sched_barrier(0);
           t0 = n0;
           t1 = n1;
         }

@@ -26,7 +26,7 @@ SQ_KERNELS = {
     "kpp_pass": "kpp_pass_kernel<",
     "lloyd_pass": "lloyd_pass_kernel<",
     "lloyd_mark": "lloyd_mark_kernel",
-    "gather": "gather_kernel<true>",
+    "gather": "gather_kernel<true, false>",
     "col_stats_rows": "col_stats_rows_kernel",
     "nz_stats": "nz_stats_u16_kernel",
     "sample_map": "sample_map_kernel",

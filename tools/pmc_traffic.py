@@ -41,12 +41,17 @@ KERNELS = {
     "lloyd_mark": "lloyd_mark_kernel",
     "sample_map": "sample_map_kernel",
     "col_stats": "col_stats_rows_kernel",
-    "gather": "gather_kernel<true>",
+    "gather": "gather_kernel<true, false>",
     "nz_stats": "nz_stats_u16_kernel",
     "mask_scatter": "mask_scatter_kernel",
 }
-# not wide coalesced streams: random rows / atomics, and 4-byte loads (col_stats)
-UNCALIBRATED = {"gather", "blur_sample", "sample_map", "lloyd_list", "lloyd_list_f64", "col_stats"}
+# not wide coalesced streams: random rows / atomics, and 4-byte loads (col_stats).
+# The gather was calibrated in round 4 (tools/gather_calib.py,
+# profiles/r04/gather_calib/): the same kernel over a sequential draw pattern
+# reads FETCH_SIZE x 2 = 2.13 GB for 2.18 GB of algorithmic reads, so the x2
+# correction holds for it; over config 2's random draws x2 gives 6.17 GB =
+# two 128-B lines per straddling 120-B row plus one per random rank lookup.
+UNCALIBRATED = {"blur_sample", "sample_map", "lloyd_list", "lloyd_list_f64", "col_stats"}
 
 
 def per_launch(path, pat):
