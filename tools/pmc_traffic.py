@@ -33,6 +33,7 @@ KERNELS = {
     "kpp_step1_f64": "kpp_pass_kernel<64, 4, 1>",
     "kpp_step_f64": "kpp_pass_kernel<64, 4, 2>",
     "lloyd_first_f64": "lloyd_pass_kernel<64, 0, 0, 1>",
+    "lloyd_first_w2": "lloyd_first_w2_kernel",
     "lloyd_tile_f64": "lloyd_pass_kernel<64, 0, 1, 1>",
     "lloyd_queue_f64": "lloyd_pass_kernel<64, 0, 2, 1>",
     "lloyd_final_f64": "lloyd_pass_kernel<64, 1, 0, 1>",
