@@ -67,10 +67,14 @@ def hbm_budget(dev=None) -> int:
 
 
 def free_bytes(dev=None) -> int:
-    """Free HBM including what torch's caching allocator holds unused."""
+    """Free HBM including what torch's caching allocator holds unused.  (The
+    allocator's two counters are read from its raw statistics: the public
+    memory_reserved / memory_allocated flatten ~300 statistics into a dict
+    each call, ~0.1 ms apiece, on the host path between the prep and the fit.)"""
     dev = torch.cuda.current_device() if dev is None else dev
     free, _ = torch.cuda.mem_get_info(dev)
-    return int(free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))
+    st = torch.cuda.memory.memory_stats_as_nested_dict(dev)
+    return int(free + st["reserved_bytes"]["all"]["current"] - st["allocated_bytes"]["all"]["current"])
 
 
 class Residency:
