@@ -530,6 +530,8 @@ class mxif_labeler(tissue_labeler):
         off = 0
         paths = []
         totals = []
+        draws = []  # (row offset, rows, rank draws, rank base): the rows' slide order, for a spatial row sort
+        rank_base = 0
         for n_img, (im, batch, (r2p, M), S) in enumerate(
                 zip(images, self.image_df["batch_names"], ranks, counts)):
             if n_img > 0:
@@ -548,6 +550,7 @@ class mxif_labeler(tissue_labeler):
                 else:
                     D.gather_rows(D.as_float32(im._materialize()), feat, idx, r2p, X[off:off + S],
                                   img_stats[n_img], accumulate=False, absmax=xmax)
+                draws.append((off, S, idx, rank_base))
                 del idx
             else:
                 # seed(16) then choice(M, 0) draws nothing: the global state
@@ -556,6 +559,7 @@ class mxif_labeler(tissue_labeler):
             r2p = None
             ranks[n_img] = (None, M)
             off += S
+            rank_base += M
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))
         self._batch_counts = counts  # merged_batch_labels is built on first access
@@ -574,6 +578,7 @@ class mxif_labeler(tissue_labeler):
         mu, inv = self.scaler.affine()
         self._rows = DeviceRows(X, mu, inv, feature_var=self.scaler.var_ * inv * inv,
                                 xmax_local=host[1])
+        self._rows.draws = draws
         self._cluster_host = None
 
     def _image_list(self):

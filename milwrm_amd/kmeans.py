@@ -46,6 +46,23 @@ class DeviceRows:
         # (mw_col_stats_absmax beside the scaler statistics), else a pass
         self._xmax_local = None if xmax_local is None else np.asarray(xmax_local, np.float32)
         self.qexp_dev = None  # fixed-point exponents of the Lloyd M-step (int32, device)
+        # the rows' draws (prep_cluster_data: [(row offset, rows, rank draws,
+        # rank base)]): their order in the slides, for spatial_order()
+        self.draws = None
+
+    def spatial_order(self):
+        """The permutation that puts the rows in slide (pixel) order, or None
+        when the draws are not known.  Rows of neighbouring pixels have
+        neighbouring values, so the rows the Lloyd bounds leave undecided (near
+        domain boundaries) come in runs: the list passes' row gathers then
+        read runs of consecutive rows instead of scattered ones."""
+        if not self.draws or sum(S for _, S, _, _ in self.draws) != self.S:
+            return None
+        keys = torch.empty(self.S, dtype=torch.int64, device=self.X.device)
+        for off, S, idx, base in self.draws:
+            keys[off:off + S].copy_(idx)
+            keys[off:off + S] += base
+        return torch.sort(keys, stable=True)[1]
 
     def _affine(self):
         if self._dev_affine is None:  # one staged copy (the C fit driver uploads its own)
@@ -346,6 +363,8 @@ KIND_FIRST, KIND_TILE, KIND_QUEUE, KIND_LIST, KIND_DENSE = 0, 1, 2, 4, 5
 # against 0.70 s with the bounded passes (4.8 ms per dense launch over all
 # fits vs 2.6-2.9 ms per list launch)
 DENSE_MIN_FITS = int(os.environ.get("MW_LLOYD_DENSE_MIN", "3"))
+# fit_many's Lloyd passes over the rows in slide order (DeviceRows.spatial_order)
+SWEEP_SORT = os.environ.get("MW_SWEEP_SORT", "1") != "0"
 USE_DENSE = os.environ.get("MW_LLOYD_DENSE", "0") == "1"
 # the few-undecided pass: kList (bound test and list in one launch, the listed
 # rows in a second) unless MW_LLOYD_LIST=0 (kQueue: both phases chunk by chunk
@@ -622,8 +641,25 @@ def fit_many(rows: DeviceRows, k_values, random_state=None, comm=None, **kw):
     tols = {km._tol for km in models}
     max_iters = {km.max_iter for km in models}
     assert len(tols) == 1 and len(max_iters) == 1
-    res = lloyd_fits(rows, inits, max_iters.pop(), tols.pop(), False, comm)
+    # the Lloyd passes over the rows in slide order (same scaler and fixed
+    # point: the M-step sums are exact integers and every other output is per
+    # row, so the fits are bit for bit those over the draw order; labels go
+    # back to draw order below)
+    perm = rows.spatial_order() if (SWEEP_SORT and len(models) > 1) else None
+    lrows = rows
+    if perm is not None:
+        lrows = DeviceRows(rows.X.index_select(0, perm), rows.mu, rows.inv, feature_var=rows._feature_var,
+                           xmax_local=rows._xmax_local)
+        lrows.xmax, lrows.qexp_dev = rows.xmax, rows.qexp_dev
+        if rows.qexp_dev is not None:
+            lrows.qexp = rows.qexp
+    res = lloyd_fits(lrows, inits, max_iters.pop(), tols.pop(), False, comm)
+    del lrows
     for km, (labels, inertia, centers, n_iter) in zip(models, res):
+        if perm is not None:
+            back = torch.empty_like(labels)
+            back[perm] = labels
+            labels = back
         km._set_fitted(rows, labels, inertia, centers, n_iter)
     return models
 

@@ -96,3 +96,26 @@ def test_kpp_indices_wide_rows(gpu, C):
             km = KMeans(n_clusters=k, random_state=18).fit(rows)
         _, idx = O.kmeans_plusplus(Xs, k, np.random.RandomState(18))
         np.testing.assert_array_equal(km.init_indices_, idx, err_msg=f"F={C} k={k}")
+
+
+@pytest.mark.timeout(300)
+def test_sweep_in_slide_order_equals_draw_order(gpu, monkeypatch):
+    """fit_many runs the Lloyd passes over the rows in slide order
+    (DeviceRows.spatial_order) and puts the labels back in draw order: every
+    fit bitwise equal to the passes over the draw order (labels, centers,
+    n_iter, inertia), k = 2..20."""
+    from milwrm_amd import kmeans as KM
+
+    rows = _rows(30, 1024)
+    assert rows.spatial_order() is not None
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(KM, "SWEEP_SORT", flag)
+        with contextlib.redirect_stdout(sys.stderr):
+            fits = KM.fit_many(rows, list(range(2, 21)), random_state=18)
+        out[flag] = [(np.asarray(m.labels_).copy(), m.cluster_centers_.copy(), m.n_iter_, m.inertia_) for m in fits]
+    for k, a, b in zip(range(2, 21), out[False], out[True]):
+        assert a[2] == b[2], f"k={k} n_iter"
+        assert a[3] == b[3], f"k={k} inertia"
+        np.testing.assert_array_equal(b[0], a[0], err_msg=f"k={k} labels")
+        np.testing.assert_array_equal(b[1], a[1], err_msg=f"k={k} centers")
