@@ -17,9 +17,7 @@
 
 namespace mw {
 
-#ifndef MW_ASSIGN_WPS
-#define MW_ASSIGN_WPS 1
-#endif
+constexpr int kAssignWPS = 1;  // label pass: minimum workgroups per CU (launch bound)
 
 static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -109,7 +107,7 @@ __host__ __device__ inline size_t assign_wave_bytes_xl(int k, int C, int CMAX) {
 // Per-block record: [sum conf k | count k] (fp64, fixed combine order).
 // Waves stream 64-pixel tiles (64*C floats) with the next tile in flight.
 template <int CMAX, int KS, bool SC, bool XL = false>
-__global__ void __launch_bounds__(256, MW_ASSIGN_WPS) assign_kernel(const float* __restrict__ img, int C,
+__global__ void __launch_bounds__(256, kAssignWPS) assign_kernel(const float* __restrict__ img, int C,
                                                      const int32_t* __restrict__ feat, int F,
                                                      const float* __restrict__ ga,
                                                      const float* __restrict__ gb,

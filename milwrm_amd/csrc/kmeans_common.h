@@ -137,10 +137,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // chain (even features in .x, odd in .y, then .x + .y) is the same fp32
 // operation sequence as a one-center loop, so the result does not depend on
 // the blocking.
-#ifndef MW_KAHEAD
-#define MW_KAHEAD 1
-#endif
-constexpr int kAhead = MW_KAHEAD;  // center pairs in flight ahead of their FMAs
+constexpr int kAhead = 1;  // center pairs in flight ahead of their FMAs
 template <int NP, int KS, int P>
 __device__ __forceinline__ void nc_read(uint32_t base, f2v (&c)[4]) {
   c[0] = ds_read8<P * KS * 8>(base);

@@ -247,10 +247,7 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
 #pragma unroll
         for (int c = 0; c < T; ++c) dot[c] = fma(xs, q.c[c], dot[c]);
       };
-#ifndef MW_KPP_SPIPE
-#define MW_KPP_SPIPE 64  // FMAX from which the pipelined form below is used
-#endif
-      if constexpr (FMAX >= MW_KPP_SPIPE) {
+      if constexpr (FMAX >= 64) {  // (FMAX = 64: the pipelined form below)
         // the row's feature pairs into registers first (one LDS wait), then
         // per pair: wait for the table loads issued one pair earlier (nothing
         // else is outstanding on the shared LDS/scalar counter), issue the next

@@ -92,10 +92,9 @@ __host__ __device__ inline size_t lloyd_tile_bytes(int FMAX, int F) {
   return (((size_t)64 * F + (FMAX - F) + 3) & ~(size_t)3) * 4;
 }
 
-#ifndef MW_LLOYD_CHUNK
-#define MW_LLOYD_CHUNK 2048  // 4096: 2 blocks per CU (LDS), the sweep's queue passes 15 % slower
-#endif
-constexpr int kChunk = MW_LLOYD_CHUNK;  // rows per bound-test chunk (kQueue passes): queue of u16 offsets
+// rows per bound-test chunk (kQueue passes): queue of u16 offsets (4096: 2
+// blocks per CU for the LDS, the sweep's queue passes 15 % slower)
+constexpr int kChunk = 2048;
 static_assert(kChunk % 1024 == 0, "chunk = whole 4-wave x 256-row groups");
 
 // small per-block LDS state (size a multiple of 16 bytes)
