@@ -23,7 +23,8 @@ import torch
 
 from . import device as D
 from .assign import (assign_image, assign_rows, banded_assign_image, blur_assign_image, dm_total,
-                     domain_means, domain_sse_deferred, domain_sse_image, domain_sse_rows)
+                     domain_means, domain_sse_deferred, domain_sse_image, domain_sse_rows,
+                     LabelPassQC)
 from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
@@ -160,8 +161,10 @@ def _domain_stats(image, use_path, scaler, centroids, features, tissue_ID):
         sigma, truncate = image._pending_blur
         inv_mean, p = image._pending
         return domain_sse_deferred(image._source() or image._device(), sigma, inv_mean, p, feats, mu,
-                                   inv, centroids, tissue_ID, truncate=truncate)
-    return domain_sse_image(D.as_float32(image._materialize()), feats, mu, inv, centroids, tissue_ID)
+                                   inv, centroids, tissue_ID, truncate=truncate,
+                                   colmax=getattr(image, "_xbound", None))
+    return domain_sse_image(D.as_float32(image._materialize()), feats, mu, inv, centroids, tissue_ID,
+                            colmax=getattr(image, "_xbound", None))
 
 
 def estimate_percentage_variance_mxif(image, use_path, scaler, centroids, features, tissue_ID):
@@ -235,10 +238,30 @@ def _check_rows_fit(S: int, F: int, dev) -> None:
             f"slide by row bands, milwrm_amd.bands) or lower fract")
 
 
-def _assign_img(image: img, features, centers, scaler):
+def _assign_img(image: img, features, centers, scaler, qc=False):
+    """(labels, confidences, per-domain records[, QC sums]) of one image: the
+    QC sums of ``_domain_stats`` as extra outputs of the same pass when
+    ``qc`` (a whole slide with a known pixel bound, ``img._blur_bound``;
+    else None: the estimators run their own pass later)."""
+    res = _assign_img_(image, features, centers, scaler, qc)
+    if not qc:
+        return res
+    lab, conf, dom, q = res
+    return lab, conf, dom, (q.result() if q is not None else None)
+
+
+def _assign_img_(image: img, features, centers, scaler, qc):
     feats = image._features(features)
     mu, inv = scaler.affine()
     centers = np.asarray(centers, dtype=np.float64)
+    band = getattr(image, "_band", None)
+    bound = getattr(image, "_xbound", None)
+    q = LabelPassQC(feats, image.n_ch, mu, inv, centers, bound) if (
+        qc and band is None and bound is not None) else None
+
+    def out(r):
+        return r if not qc else (*r, q)
+
     if image._pending_blur is not None:
         # deferred blur (D.defer_blur: the fp32 blurred slide does not fit
         # HBM): blur band by band into a reused buffer and label each band
@@ -253,23 +276,27 @@ def _assign_img(image: img, features, centers, scaler):
         # resident raw slide, or (not resident) its stream.RowSource read band by band
         raw = image._source() or image._device()
         fusable = band is None and feats == list(range(image.n_ch))
-        if how == "fused" and fusable:
+        if how == "fused" and fusable:  # no fp32 band: the QC sums are left to the estimators
             res = blur_assign_image(raw, sigma, inv_mean, p, mu, inv, centers, image._mask_device(),
                                     truncate=truncate)
+            q = None
         if res is None:
             res = banded_assign_image(raw, sigma, inv_mean, p, feats, mu, inv, centers,
-                                      image._mask_device(), truncate=truncate, out_rows=out_rows)
+                                      image._mask_device(), truncate=truncate, out_rows=out_rows, qc=q)
         if res is None and how != "fused" and fusable:  # not even a 16-row fp32 band fits
             res = blur_assign_image(raw, sigma, inv_mean, p, mu, inv, centers, image._mask_device(),
                                     truncate=truncate)
+            q = None
         if res is not None:
-            return res
+            return out(res)
     src = D.as_float32(image._materialize())
-    band = getattr(image, "_band", None)
     if band is not None:  # label the band rows only (milwrm_amd.bands)
-        return assign_image(src[band.rows], feats, mu, inv, centers,
-                            D.padded_mask(image._mask_device()[band.rows].contiguous()))
-    return assign_image(src, feats, mu, inv, centers, image._mask_device())
+        return out(assign_image(src[band.rows], feats, mu, inv, centers,
+                                D.padded_mask(image._mask_device()[band.rows].contiguous())))
+    res = assign_image(src, feats, mu, inv, centers, image._mask_device())
+    if q is not None:  # the slide is resident: its QC sums from the same fp32 pixels
+        q.band(src, res[0])
+    return out(res)
 
 
 def _gather_deferred(image: img, feat, idx, r2p, X_out) -> bool:
@@ -388,6 +415,7 @@ class tissue_labeler:
             print("Overriding optimal k value with k={}.".format(k))
             self.k = k
         self.random_state = random_state
+        self._qc_stats = None  # QC sums a label pass took belong to the previous centers
         print("Performing k-means clustering with {} target clusters".format(self.k))
         self.kmeans = KMeans(n_clusters=self.k, random_state=random_state).fit(
             self._device_rows(), comm=self._comm)
@@ -587,9 +615,13 @@ class mxif_labeler(tissue_labeler):
         return list(self.image_df["Img"])
 
     def label_tissue_regions(self, k=None, alpha=0.05, plot_out=True, random_state=18, n_jobs=-1,
-                             comm=None):
+                             comm=None, qc=False):
         """MILWRM.py:1747-1794 plus the fused confidence pass (MILWRM.py:389-450
-        is computed in the same sweep over each image)."""
+        is computed in the same sweep over each image).  ``qc``: also take the
+        QC sums behind ``plot_percentage_variance_explained`` /
+        ``plot_mse_mxif`` (MILWRM.py:280-333, 453-515) from the same pass --
+        band by band on a deferred-blur slide, so the slide is not blurred
+        again for them; the same bits as the estimators' own passes."""
         if comm is not None:
             self._comm = comm
         if k is None:
@@ -598,15 +630,114 @@ class mxif_labeler(tissue_labeler):
                                 n_jobs=n_jobs)
         self.find_tissue_regions(k=k, random_state=random_state)
         print("Creating tissue_ID images for image objects...")
-        labs, confs, doms = [], [], []
+        labs, confs, doms, qcs = [], [], [], []
         for image in self._image_list():
-            lab, conf, dom = _assign_img(image, self.model_features, self.kmeans.cluster_centers_,
-                                         self.scaler)
-            labs.append(lab)
-            confs.append(conf)
-            doms.append(dom)
+            res = _assign_img(image, self.model_features, self.kmeans.cluster_centers_, self.scaler,
+                              qc=qc)
+            labs.append(res[0])
+            confs.append(res[1])
+            doms.append(res[2])
+            qcs.append(res[3] if qc else None)
         self._labels_dev, self._conf_dev, self._dom_dev = labs, confs, doms
+        self._qc_stats = qcs
         self.tissue_IDs = _LazyHostList(labs, _labels_to_host)
+
+    def _image_qc_stats(self) -> list:
+        """Per image, the QC sums (``_domain_stats``) of the current labelling:
+        those the label pass took (``label_tissue_regions(qc=True)``), else an
+        estimator pass over the image."""
+        cached = getattr(self, "_qc_stats", None) or []
+        out = []
+        for i, (image, tid) in enumerate(zip(self.image_df["Img"], self.tissue_IDs)):
+            s = cached[i] if i < len(cached) else None
+            if s is None:
+                s = _domain_stats(image, self.use_paths, self.scaler, self.kmeans.cluster_centers_,
+                                  self.model_features, tid)
+            out.append(s)
+        return out
+
+    def percentage_variance_images(self) -> list:
+        """S^2 per image: estimate_percentage_variance_mxif (MILWRM.py:280-333)
+        of each image under the current labelling, as
+        ``plot_percentage_variance_explained`` (:1796-1866) computes them."""
+        return [np.float64(np.sum(s["sse"])) / dm_total(s) * 100 for s in self._image_qc_stats()]
+
+    def mse_images(self) -> dict:
+        """{domain: [per-feature MSE for each image]}: estimate_mse_mxif
+        (MILWRM.py:453-515) as ``plot_mse_mxif`` (:1902-2011) computes it."""
+        k = int(self.k)
+        per = []
+        for s in self._image_qc_stats():
+            cnt = s["count"][:k, None]
+            per.append(np.where(cnt > 0, s["sse"][:k] / np.maximum(cnt, 1), 0.0))
+        return {i: [m[i] for m in per] for i in range(k)} if per else {}
+
+    def plot_percentage_variance_explained(self, fig_size=(5, 5), R_square=False, save_to=None):
+        """MILWRM.py:1796-1866: per image, the percentage of variance the
+        clustering explains (R^2 = 100 - S^2) or leaves (S^2), as a scatter
+        with the mean as a dashed line."""
+        import matplotlib.pyplot as plt
+
+        S = self.percentage_variance_images()
+        vals = [100 - v for v in S] if R_square else S
+        fig = plt.figure(figsize=fig_size)
+        plt.scatter(range(len(vals)), vals, color="black")
+        plt.xlabel("images")
+        plt.ylabel("percentage variance explained by Kmeans")
+        plt.ylim((0, 100))
+        plt.axhline(y=np.mean(vals), linestyle="dashed", linewidth=1, color="black")
+        fig.tight_layout()
+        if save_to:
+            plt.savefig(fname=save_to, transparent=True, bbox_inches="tight", dpi=300)
+        return fig
+
+    def plot_mse_mxif(self, figsize=(5, 5), ncols=None, labels=None, legend_cols=2, titles=None,
+                      loc="lower right", bbox_coordinates=(0, 0, 1.5, 1.5), save_to=None):
+        """MILWRM.py:1902-2011: per tissue domain, a box plot over features of
+        the per-image MSE, the images as jittered dots (np.random.uniform, the
+        reference's global-RNG draws)."""
+        import matplotlib.pyplot as plt
+        from matplotlib import gridspec
+
+        assert self.kmeans is not None, "No cluster results found. Run \
+        label_tissue_regions() first."
+        mse_id = self.mse_images()
+        n_img = len(self.image_df["Img"])
+        features = self.model_features
+        if labels is None:
+            labels = range(n_img)
+        if titles is None:
+            titles = ["tissue_ID " + str(x) for x in range(self.k)]
+        n_panels = len(mse_id)
+        if ncols is None:
+            ncols = len(titles)
+        n_rows, n_cols = (1, n_panels) if n_panels <= ncols else (-(-n_panels // ncols), ncols)
+        colors = plt.cm.tab20(np.linspace(0, 1, n_img))
+        fig = plt.figure(figsize=(n_cols * figsize[0], n_rows * figsize[1]))
+        left, bottom = 0.1 / n_cols, 0.1 / n_rows
+        gs = gridspec.GridSpec(nrows=n_rows, ncols=n_cols, left=left, bottom=bottom,
+                               right=1 - (n_cols - 1) * left - 0.01 / n_cols,
+                               top=1 - (n_rows - 1) * bottom - 0.1 / n_rows)
+        for i in mse_id:
+            plt.subplot(gs[i])
+            df = pd.DataFrame.from_dict(mse_id[i])
+            plt.boxplot(df, positions=range(len(features)), showfliers=False)
+            plt.xticks(ticks=range(len(features)), labels=self.model_features, rotation=60, fontsize=8)
+            for col in df:
+                for j in range(n_img):
+                    dots = plt.scatter(col, df[col][j], s=j + 1, color=colors[j],
+                                       label=labels[j] if col == 0 else "")
+                    off = dots.get_offsets()
+                    off[:, 0] += np.random.uniform(-0.3, 0.3, off.shape[0])  # x jitter only
+                    dots.set_offsets(off)
+            plt.xlabel("marker")
+            plt.ylabel("mean square error")
+            plt.title(titles[i])
+        plt.legend(loc=loc, bbox_to_anchor=bbox_coordinates, ncol=legend_cols)
+        gs.tight_layout(fig)
+        if save_to:
+            plt.savefig(fname=save_to, transparent=True, dpi=300)
+        return fig
 
     def plot_tissue_ID_proportions_mxif(self, tID_labels=None, slide_labels=None, figsize=(5, 5),
                                         cmap="tab20", save_to=None):

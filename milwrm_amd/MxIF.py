@@ -64,6 +64,8 @@ class img:
         self._dev = None            # HWC device tensor (authoritative when set)
         self._pending = None        # (inv_mean fp32 device tensor, pseudoval) deferred log_normalize
         self._pending_blur = None   # (sigma, truncate) deferred gaussian (fused-epilogue mode)
+        self._lognorm_host = None   # (inv_mean fp32 host array, pseudoval) of the pending log_normalize
+        self._xbound = None         # per-channel bound on |pixel| of blur(lognorm(raw)), see _blur_bound
         self.n_ch = img_arr.shape[2] if img_arr.ndim > 2 else 1
         if channels is None:
             self.ch = ["ch_{}".format(x) for x in range(self.n_ch)]
@@ -163,6 +165,8 @@ class img:
         obj._dev = None
         obj._pending = None
         obj._pending_blur = None
+        obj._lognorm_host = None
+        obj._xbound = None
         obj._src = src
         obj._hsrc = None
         obj._revert = None
@@ -266,6 +270,8 @@ class img:
         self._hsrc = None
         self._pending = None
         self._pending_blur = None
+        self._lognorm_host = None
+        self._xbound = None
 
     @property
     def mask(self):
@@ -351,6 +357,8 @@ class img:
         obj._dev = tensor
         obj._pending = None
         obj._pending_blur = None
+        obj._lognorm_host = None
+        obj._xbound = None
         obj.n_ch = int(tensor.shape[2])
         obj.ch = channels if channels is not None else ["ch_{}".format(x) for x in range(obj.n_ch)]
         obj._mask = None
@@ -432,29 +440,9 @@ class img:
             if mode != "nearest" or kwargs:
                 raise NotImplementedError(f"gaussian options {dict(mode=mode, **kwargs)} "
                                           "(only mode='nearest' is implemented)")
-            if self._pending_blur is None and self._source() is not None:
-                # not resident: the blur runs inside every pass over the
-                # streamed bands (stream.blur_gather, the banded label pass)
-                self._pending_blur = (float(sigma), truncate)
-                if self._pending is None:
-                    self._pending = (None, 1.0)  # no log-normalise before this blur
-                self._host64 = None
-                return
-            src = self._materialize() if self._pending_blur is not None else self._device()
-            if self._pending is not None and src.dim() == 3 and (
-                    D.defer_blur(*src.shape) or not self._may_hold(src.numel() * 4)):
-                # fused-epilogue mode: the subsample gather and the label pass
-                # recompute the blur from the raw slide (D.defer_blur, or the
-                # fp32 copy of a host-backed slide would exceed the HBM budget)
-                self._pending_blur = (float(sigma), truncate)
-                self._host64 = None
-                return
-            self._pending_blur = (float(sigma), truncate)
-            if self._pending is None:
-                self._pending = (None, 1.0)
-            inv, p = self._pending
-            self._transformed(lambda: D.blur(src, float(sigma), inv_mean=inv, pseudoval=p,
-                                             truncate=truncate))
+            bound = self._blur_bound()
+            self._blur_(float(sigma), truncate)
+            self._xbound = bound
         elif filter_name == "median":
             # The reference's median branch calls np.ones(sigma, sigma), which
             # raises for any integer sigma (MxIF.py:403); keep that behaviour.
@@ -467,6 +455,72 @@ class img:
             raise NotImplementedError("bilateral filter is outside the MI355X hot path")
         else:
             raise Exception("filter name should be either gaussian, median or bilateral")
+
+    def _raw_int_max(self):
+        """The largest value the current pixels' element type holds when they
+        are a raw uint8 / uint16 slide (device, host or streamed), else None."""
+        if self._pending_blur is not None:
+            return None
+        if self._dev is not None:
+            t = self._dev.dtype
+        elif self._host is not None:
+            t = {np.dtype(np.uint8): torch.uint8, np.dtype(np.uint16): torch.int16}.get(self._host.dtype)
+        elif self._src is not None:
+            t = self._src.dtype
+        else:
+            return None
+        return {torch.uint8: 255.0, torch.int16: 65535.0}.get(t)  # int16 storage = uint16 bits
+
+    def _blur_bound(self):
+        """Per-channel bound on |x| of blur(lognorm(raw)) for a raw integer
+        slide, known before any pixel is blurred: log10(x inv + p) is monotone
+        in x in [0, dtype max], and the gaussian is a convex combination, so
+        |x| <= max(|log10 p|, |log10(max inv + p)|) (max itself without a
+        log_normalize), with slack for the fp32 arithmetic.  The exact QC sums
+        take their fixed point from it (milwrm_amd.assign._DomainSSE): the
+        label pass can then add each band's sums as it labels it, and the
+        standalone estimators give the same bits without a first pass for the
+        column maxima.  None when the pixels are not such a slide."""
+        mx = self._raw_int_max()
+        if mx is None:
+            return None
+        if self._pending is None:
+            return np.full(self.n_ch, mx * (1 + 1e-3))
+        if self._lognorm_host is None:
+            return None
+        inv, p = self._lognorm_host
+        if not (np.isfinite(p) and p > 0):
+            return None
+        with np.errstate(invalid="ignore", over="ignore"):
+            hi = np.log10(mx * inv.astype(np.float64) + p)
+        return np.maximum(abs(np.log10(p)), np.abs(hi)) * (1 + 1e-3) + 1e-30
+
+    def _blur_(self, sigma: float, truncate: float):
+        """The gaussian branch of ``blurring``: deferred (streamed slide, or the
+        fp32 copy would not fit) or materialised."""
+        if self._pending_blur is None and self._source() is not None:
+            # not resident: the blur runs inside every pass over the
+            # streamed bands (stream.blur_gather, the banded label pass)
+            self._pending_blur = (sigma, truncate)
+            if self._pending is None:
+                self._pending = (None, 1.0)  # no log-normalise before this blur
+            self._host64 = None
+            return
+        src = self._materialize() if self._pending_blur is not None else self._device()
+        if self._pending is not None and src.dim() == 3 and (
+                D.defer_blur(*src.shape) or not self._may_hold(src.numel() * 4)):
+            # fused-epilogue mode: the subsample gather and the label pass
+            # recompute the blur from the raw slide (D.defer_blur, or the
+            # fp32 copy of a host-backed slide would exceed the HBM budget)
+            self._pending_blur = (sigma, truncate)
+            self._host64 = None
+            return
+        self._pending_blur = (sigma, truncate)
+        if self._pending is None:
+            self._pending = (None, 1.0)
+        inv, p = self._pending
+        self._transformed(lambda: D.blur(src, sigma, inv_mean=inv, pseudoval=p,
+                                         truncate=truncate))
 
     def log_normalize(self, pseudoval=1, mean=None, mask=True):
         """MxIF.py:416-455: log10(x/mean_c + pseudoval) on every pixel.  The
@@ -486,7 +540,11 @@ class img:
         mean = np.asarray(mean, dtype=np.float64)
         with np.errstate(divide="ignore"):
             inv = (1.0 / mean).astype(np.float32)
+        # a raw integer slide's bound survives a pending log_normalize (_blur_bound)
+        raw = self._raw_int_max() is not None and self._pending is None and self._pending_blur is None
         self._pending = (D.h2d(inv, D.device()), float(pseudoval))
+        self._lognorm_host = (inv, float(pseudoval)) if raw else None
+        self._xbound = None
         self._host64 = None
 
     def _subsample_device(self, features, fract=0.2, random_state=16, X_out=None, stats=None,
@@ -536,6 +594,7 @@ class img:
             self.mask = D.block_mean(m, int(fact))[:, :, 0].double().cpu().numpy()
         out = D.block_mean(self._materialize(), int(fact))
         self._set_device(out)
+        self._xbound = None
 
     def _nz_stats(self):
         """Per-channel non-zero (sum, count) of the current pixels: band by

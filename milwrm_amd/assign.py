@@ -107,7 +107,7 @@ def _assign_band_rows(src, r, extra_per_row, band_rows):
 
 def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
                         inv, centers: np.ndarray, mask_u8: torch.Tensor, truncate: float = 4.0,
-                        band_rows=None, out_rows=None):
+                        band_rows=None, out_rows=None, qc: LabelPassQC | None = None):
     """``assign_image(blur(lognorm(raw)))`` for a slide whose fp32 blurred copy
     does not fit HBM: the blur is materialised one band of rows at a time
     (band plus r halo rows of input; the kernel's arithmetic per output value
@@ -119,7 +119,8 @@ def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
     one is labelled).  None when not even a 16-row band fits in half the
     free HBM.  ``out_rows`` = (r0, r1): label only those rows of ``raw`` (a
     slide band's own rows inside its halo'd array, milwrm_amd.bands); outputs
-    are (r1 - r0) x W."""
+    are (r1 - r0) x W.  ``qc``: a ``LabelPassQC`` that takes every labelled
+    band (whole slides only: ``out_rows`` None)."""
     from .stream import as_source, bands
 
     src = as_source(raw)
@@ -145,6 +146,8 @@ def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
                                D.padded_mask(mask_u8[y0:y1].contiguous()),
                                out_lab=lab[y0 - r0:y1 - r0], out_conf=conf[y0 - r0:y1 - r0])
         dom += d
+        if qc is not None:  # the band is still in the buffer: its QC sums now
+            qc.band(out[y0 - a:y1 - a], lab[y0 - r0:y1 - r0])
     D.FUSED_USED["assign_banded"] += 1
     if not src.zero_copy:
         D.FUSED_USED["assign_streamed"] += 1
@@ -308,14 +311,16 @@ def _first_pixel_scaled(img_f32, feat, mu, inv) -> np.ndarray:
 
 def domain_sse_deferred(raw, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
                         inv, centers: np.ndarray, tissue_id, truncate: float = 4.0,
-                        band_rows=None) -> dict:
+                        band_rows=None, colmax=None) -> dict:
     """``domain_sse_image(blur(lognorm(raw)), ...)`` for a slide whose fp32
     blurred copy does not fit HBM (the deferred-blur mode): the blur is
     materialised band by band (band + r halo rows of input) into one reused
     buffer, twice -- once for the column maxima that fix the fixed point,
-    once for the sums.  The sums are exact, so the result is bitwise the
-    materialised slide's (tests/test_gpu_qc.py).  ``raw``: a resident slide
-    or a ``stream.RowSource`` (read band by band, twice)."""
+    once for the sums -- or once when ``colmax`` (a per-channel bound on |x|,
+    ``img._blur_bound``) is given.  The sums are exact, so the result is
+    bitwise the materialised slide's given the same bound
+    (tests/test_gpu_qc.py).  ``raw``: a resident slide or a
+    ``stream.RowSource`` (read band by band)."""
     from .stream import as_source
     from .stream import bands as read_bands
 
@@ -342,16 +347,62 @@ def domain_sse_deferred(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
             D.blur(rb, sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
             yield y0, y1, out[y0 - a:y1 - a]
 
-    cmax = torch.zeros(C, dtype=torch.float32, device=dev)
-    pivot = None
+    acc = None
+    if colmax is None:
+        cmax = torch.zeros(C, dtype=torch.float32, device=dev)
+        pivot = None
+        for y0, y1, core in bands():
+            if pivot is None:
+                pivot = _first_pixel_scaled(core, feat, mu, inv)
+            _colmax(core, cmax, accumulate=True)
+        acc = _DomainSSE(feat, F, mu, inv, centers, pivot, D.d2h(cmax), dev)
     for y0, y1, core in bands():
-        if pivot is None:
-            pivot = _first_pixel_scaled(core, feat, mu, inv)
-        _colmax(core, cmax, accumulate=True)
-    acc = _DomainSSE(feat, F, mu, inv, centers, pivot, D.d2h(cmax), dev)
-    for y0, y1, core in bands():
+        if acc is None:  # the pivot is the slide's first pixel, as above
+            acc = _DomainSSE(feat, F, mu, inv, centers, _first_pixel_scaled(core, feat, mu, inv),
+                             colmax, dev)
         acc.add(core, lab[y0 * W:y1 * W])
     return acc.result()
+
+
+class LabelPassQC:
+    """The QC sums of ``domain_sse_image`` as extra outputs of the label pass
+    (SURVEY 8f row 3): the banded label pass hands every fp32 band it has
+    just labelled, with its labels, to ``band`` (no second blur of the
+    slide); a resident slide is handed whole.  The fixed point comes from
+    ``colmax`` (the slide's ``img._blur_bound``, known before the first band)
+    and the pivot from the slide's first pixel, as the standalone
+    ``domain_sse_image`` / ``domain_sse_deferred`` take them, so the sums are
+    the same bits as those passes'."""
+
+    def __init__(self, feat_idx, C, mu, inv, centers: np.ndarray, colmax):
+        k, F = centers.shape
+        self.feat = _check_feats(feat_idx, F, C)
+        self.mu, self.inv = mu, inv
+        self.centers = np.ascontiguousarray(centers, dtype=np.float64)
+        self.colmax = colmax
+        self.acc = None
+        self.stats = None
+        self.n_bands = 0
+
+    def band(self, core: torch.Tensor, labels_i8: torch.Tensor):
+        """Add an fp32 HWC band (the slide's rows from its first on) and its
+        int8 labels (-1 = no domain), in slide order."""
+        self.n_bands += 1
+        if self.n_bands >= 1 << 10:  # past the exact-limb budget (domain_sse_deferred): no result
+            self.acc = False
+        if self.acc is False:
+            return
+        if self.acc is None:
+            self.acc = _DomainSSE(self.feat, self.centers.shape[1], self.mu, self.inv, self.centers,
+                                  _first_pixel_scaled(core, self.feat, self.mu, self.inv),
+                                  self.colmax, core.device)
+        self.acc.add(core, labels_i8.reshape(-1))
+
+    def result(self):
+        """The ``domain_sse_image`` dict, or None (nothing added, or too many
+        bands: the estimators then run their own pass)."""
+        self.stats = self.acc.result() if self.acc else None
+        return self.stats
 
 
 def domain_sse_rows(X: np.ndarray, centers: np.ndarray, labels) -> dict:

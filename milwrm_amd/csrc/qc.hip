@@ -30,10 +30,13 @@
 // Layout: a block of 256 threads is split into floor(256/F) groups of F lanes;
 // lane f of a group owns feature f, so a wave reads whole pixels (F contiguous
 // floats for identity features) and every lane keeps its own per-domain
-// column of int64 accumulators in LDS (no atomics, no bank conflicts); eight
-// pixels' loads are issued before their updates (kQcUnroll = 8).  Per-block
-// partials go to a workspace and a second kernel folds them in a fixed order.
-// HBM-bound: n_pix * (C*4 + 1) bytes.
+// column of int64 accumulators in LDS (no atomics, no bank conflicts);
+// sixteen pixels' loads are issued before their updates (kQcUnroll = 16: 8 ->
+// 16 took a 40k^2 x 50 slide's QC sums from 202 to 171 ms, 32 measured the
+// same).  Per-block partials go to a workspace and a second kernel folds them
+// in a fixed order.  Algorithmic bytes n_pix * (C*4 + 1); it runs at ~2 TB/s,
+// bound by the three fixed-point conversions and the LDS read-modify-write of
+// every element, not by HBM.
 #include "common.h"
 
 namespace mw {
@@ -41,14 +44,26 @@ namespace mw {
 constexpr int kQcThreads = 256;
 constexpr int kQcMaxK = 20;  // LDS <= 2*20*256*8 + 4*256*8 + 20*256*4 (F = 1) = 108 KiB
 constexpr int kQcMaxBlocks = 2048;
-constexpr int kQcUnroll = 8;
+constexpr int kQcUnroll = 16;
+
+// rint(s) as a double and as an int64 for |s| < 2^51: s + 1.5 2^52 lands in
+// [2^52, 2^53), where the ulp is 1, so the add rounds s to the nearest
+// integer (ties to even, as rint) and the low mantissa bits are that integer
+// (offset by the constant's): two VALU ops instead of rint plus the
+// multi-instruction fp64 -> int64 conversion, and the same values
+__device__ __forceinline__ long long qc_rint64(double s, double& h) {
+  constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+  const double t = s + kMagic;
+  h = t - kMagic;
+  return __double_as_longlong(t) - __double_as_longlong(kMagic);
+}
 
 // two-level fixed point of v at exponent e: hi += rint(v 2^e), lo += rint(residual 2^38)
 __device__ __forceinline__ void qc_fix2(double v, int e, long long& hi, long long& lo) {
   const double s = ldexp(v, e);
-  const double h = rint(s);
-  hi += (long long)h;
-  lo += (long long)rint(ldexp(s - h, 38));  // s - h exact (|s| < 2^39)
+  double h, r;
+  hi += qc_rint64(s, h);
+  lo += qc_rint64(ldexp(s - h, 38), r);  // s - h exact (|s| < 2^39), |(s - h) 2^38| <= 2^37
 }
 
 __device__ __forceinline__ void qc_limbs(long long v, double& hi, double& lo) {

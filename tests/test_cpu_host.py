@@ -201,3 +201,28 @@ def test_stream_parse_bytes_and_host_dtypes():
     rows = hs._host_rows(1, 3)
     assert rows.dtype == torch.int16 and tuple(rows.shape) == (2, 4, 3)
     assert int(rows.view(torch.int16).to(torch.int32)[0, 0, 0]) & 0xFFFF == 60000 + 12
+
+
+def test_blur_bound_bounds_lognorm_blur():
+    """img._blur_bound (the QC fixed point's pixel bound, known before the
+    blur): |blur(lognorm(raw))| <= bound on every channel of the oracle's fp64
+    pipeline, for uint16 / uint8 slides, with and without a log_normalize;
+    None for float slides and once the pixels are no longer raw."""
+    import milwrm_amd as M
+    from oracle import milwrm_oracle as O
+
+    raw, _ = O.synth_slide(40, 48, 5, seed=11, mode="hard")
+    raw[3, 4, 1] = 65535  # the dtype max itself
+    mean = raw.reshape(-1, 5).mean(0)
+    for a, mx in ((raw, 65535.0), (np.minimum(raw, 255).astype(np.uint8), 255.0)):
+        im = M.img(a.copy())
+        assert im._raw_int_max() == mx
+        assert np.all(im._blur_bound() >= np.abs(O.gaussian_blur(a.astype(np.float64))).max((0, 1)))
+        for p in (1.0, 0.25):
+            inv = (1.0 / mean).astype(np.float32)
+            im._pending, im._lognorm_host = ("device", p), (inv, p)  # as log_normalize leaves them
+            ref = O.gaussian_blur(O.log_normalize(a, mean, pseudoval=p))
+            assert np.all(im._blur_bound() >= np.abs(ref).max((0, 1)))
+            im._lognorm_host = None  # a pending transform of pixels that were not raw
+            assert im._blur_bound() is None
+    assert M.img(raw.astype(np.float32))._blur_bound() is None

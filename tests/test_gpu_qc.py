@@ -343,3 +343,56 @@ def test_qc_nonfinite_feature_gives_nan(gpu):
     for d in range(3):
         assert np.isnan(mse[d][0][2])
         np.testing.assert_array_equal(np.delete(mse[d][0], 2), np.delete(clean[d][0], 2))
+
+
+@pytest.mark.parametrize("mode", ["materialised", "banded", "fused"])
+def test_label_pass_qc_equals_estimators(gpu, golden, monkeypatch, mode):
+    """label_tissue_regions(qc=True): the QC sums behind
+    plot_percentage_variance_explained / plot_mse_mxif (MILWRM.py:1796-2011)
+    taken as extra outputs of the label pass -- the resident slide whole, a
+    deferred-blur slide band by band from the label pass's own fp32 bands
+    (21-row bands: no second blur) -- are bitwise the estimators' own passes
+    (fixed point from the raw slide's bound, img._blur_bound, in both).  The
+    fused label epilogue has no fp32 band: the estimators run their pass and
+    give the same bits.  S^2 against the oracle's fp64 restatement on the same
+    labels."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import milwrm_amd as M
+    from milwrm_amd import MILWRM as MW
+
+    g = golden("qc_small")
+    monkeypatch.setenv("MW_ASSIGN_BAND_ROWS", "21")
+    monkeypatch.setenv("MW_FUSED_BLUR", "0" if mode == "materialised" else "1")
+    monkeypatch.setenv("MW_DEFERRED_ASSIGN", "fused" if mode == "fused" else "band")
+    imgs = [M.img(r.copy(), mask=m.copy()) for r, m in zip(g["raw"], g["masks"])]
+    ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
+    batches = ["b1", "b1", "b2"]
+    df = pd.DataFrame({"Img": imgs, "batch_names": batches,
+                       "mean estimators": list(ests), "pixels": list(pix)})
+    lab = M.mxif_labeler(df)
+    lab.prep_cluster_data(features=FEATS, sigma=2, fract=0.2)
+    assert all((im._pending_blur is not None) == (mode != "materialised") for im in imgs)
+    assert all(im._xbound is not None for im in imgs)
+    lab.label_tissue_regions(k=4, plot_out=False, random_state=18, qc=True)
+    taken = [s is not None for s in lab._qc_stats]
+    assert all(taken) if mode != "fused" else not any(taken)
+    pv = lab.percentage_variance_images()
+    mse = lab.mse_images()
+    cents = lab.kmeans.cluster_centers_
+    tids = list(lab.tissue_IDs)
+    est_pv = [MW.estimate_percentage_variance_mxif(im, False, lab.scaler, cents, FEATS, t)
+              for im, t in zip(imgs, tids)]
+    est_mse = MW.estimate_mse_mxif(imgs, False, tids, lab.scaler, cents, FEATS, 4)
+    np.testing.assert_array_equal(pv, est_pv)
+    for i in range(4):
+        np.testing.assert_array_equal(np.array(mse[i]), np.array(est_mse[i]))
+    assert lab.plot_percentage_variance_explained(R_square=True) is not None
+    assert lab.plot_mse_mxif() is not None
+    e_p = [O.non_zero_mean(r) for r in g["raw"]]
+    bm = O.batch_means([e for e, _ in e_p], [p for _, p in e_p], batches)
+    for i, r in enumerate(g["raw"]):
+        pre = O.gaussian_blur(O.log_normalize(r, bm[batches[i]]))
+        ref = O.percentage_variance_mxif(pre, FEATS, cents, lab.scaler.mean_, lab.scaler.scale_, tids[i])
+        assert abs(pv[i] - ref) <= 1e-5 * abs(ref), f"image {i}"
