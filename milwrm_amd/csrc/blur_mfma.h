@@ -182,6 +182,8 @@ __host__ __device__ __forceinline__ int blur_h16_unit(int x, int ct) {
 // log-normalised values are scaled by 2^8 before the split (the lo half stays
 // clear of f16 subnormals), the horizontal taps by 2^16; the vertical taps
 // take the 2^-24 back (exact: powers of two)
+// cache policy of the blurred-row stores (buffer aux bits; 2 = nt: streaming)
+constexpr int kBlurStoreAux = 2;
 constexpr bool kBlurH16 = true;   // log-normalised input: horizontal pass on f16 hi/lo products
 constexpr float kH16XS = 256.f, kH16TS = 65536.f, kH16VS = 1.f / 16777216.f;
 
@@ -462,7 +464,7 @@ __global__ void __launch_bounds__(64 * BT * CT, 4) blur_mfma_kernel(const T* __r
     const f4m v = *reinterpret_cast<const f4m*>(s_stg + stg_buf * STG + 4 * t);
     const __amdgpu_buffer_rsrc_t ro =
         blur_rsrc(out + ((int64_t)(valid ? yo - bg.r0 : 0) * W + x0) * C, valid ? out_bytes : 0u);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4m, v), ro, t * 16, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4m, v), ro, t * 16, 0, kBlurStoreAux);
   };
 
   // kEpiSample / kEpiAssign on the output row staged at step s-1 (buffer s & 1)

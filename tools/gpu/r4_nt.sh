@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-4 A/B: non-temporal (nt) blurred-row stores (new lib) against the
+# committed lib (abv/lib_head.so): blur parity tests, config 2 x2 alternating, config 5 x1 each.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/${1:-r4nt}; mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+T="--timeout-method thread"
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 $T -m gpu -k "blur or gauss or prep" > $OUT/tests.log 2>&1 || exit 1
+for r in 1 2; do
+  timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-design-point > $OUT/c2_new$r.json 2> $OUT/c2_new$r.err || exit 1
+  MW_LIB=abv/lib_head.so timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-design-point > $OUT/c2_head$r.json 2> $OUT/c2_head$r.err || exit 1
+done
+timeout -k 10 300 python -u bench.py --size 40000 --channels 50 --steps 2 --warmup 1 --no-cpu-baseline > $OUT/c5_new.json 2> $OUT/c5_new.err || exit 1
+MW_LIB=abv/lib_head.so timeout -k 10 300 python -u bench.py --size 40000 --channels 50 --steps 2 --warmup 1 --no-cpu-baseline > $OUT/c5_head.json 2> $OUT/c5_head.err || exit 1
+echo "[nt] done"
