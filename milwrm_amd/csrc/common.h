@@ -53,6 +53,31 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// Lane i of each 16-lane row takes lane i + N of the row (DPP row_shl:N; lanes
+// past the row read 0: bound_ctrl).  Two 32-bit DPP moves for a double.
+template <int N>
+__device__ __forceinline__ double dpp_row_shl(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x100 + N, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x100 + N, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// wave_sum's value in lane 0 only, bit for bit: at the level of offset o lane
+// 0's tree needs lane i + o in lanes i < o, which is their xor partner, so the
+// same additions happen in the same order; offsets 32 and 16 cross rows (LDS
+// permutes, as wave_sum), 8, 4, 2, 1 are DPP row shifts (VALU, no LDS
+// round trip in the dependent chain)
+__device__ __forceinline__ double wave_sum_lane0(double v) {
+  v += __shfl_xor(v, 32, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += dpp_row_shl<8>(v);
+  v += dpp_row_shl<4>(v);
+  v += dpp_row_shl<2>(v);
+  v += dpp_row_shl<1>(v);
+  return v;
+}
+
 // Block-wide sum of one value per thread; result valid in thread 0.
 // `scratch` must hold blockDim.x/64 elements.  Fixed combine order.
 template <typename T>

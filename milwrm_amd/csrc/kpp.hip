@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
       const double m = MODE == 0 ? d[0] : (cd < d[c] ? cd : d[c]);
       const double mv = valid ? m : 0.0;
       acc[c] += mv;
-      const double ts = wave_sum(mv);
+      const double ts = wave_sum_lane0(mv);  // lane 0 stores it
       if (lane == 0) tsum_new[(size_t)c * NTL + (r0 >> 6)] = ts;
     }
   }
