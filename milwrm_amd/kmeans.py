@@ -379,8 +379,10 @@ def lloyd_ws_bytes(S: int, k: int, F: int) -> int:
 # a mode-0 pass streams every row (kTile) while the previous pass recomputed
 # more than this fraction of the rows, else only the undecided ones (kQueue):
 # the k = 2..20 sweep at 10k^2 x 30 (tools/sweep_bench.py) took 0.77 / 0.69 s
-# at 0.12 / 0.3 (round 1: 1.05 / 1.03 / 0.90 s at 0.03 / 0.06 / 0.12); the
-# single k = 8 fit of the bench is neutral
+# at 0.12 / 0.3 (round 1: 1.05 / 1.03 / 0.90 s at 0.03 / 0.06 / 0.12).  Round
+# 4, config 2 (profiles/r04/tried/queue_below): fit 7.44 ms at 0.3 against
+# 7.6-8.1 at 0.1 / 0.2 / 0.5 / 0.7 / 1.0; the I = 17 design point 14.6 at 0.2,
+# 14.9 at 0.3; the sweep 0.63 s at 0.3 / 0.5, 0.66 at 0.2
 QUEUE_BELOW = float(os.environ.get("MW_LLOYD_QUEUE_BELOW", "0.3"))
 # KMeans.fit through the C++ driver (mw_kmeans_fit) where it applies; MW_KMEANS_C=0
 # keeps the Python loop (A/B and the per-pass trace)
