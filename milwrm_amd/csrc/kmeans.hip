@@ -446,6 +446,7 @@ int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F, cons
   if (C <= 8) { MW_ASK(8) }
   else if (C <= 16) { MW_ASK(16) }
   else if (C <= 32) { MW_ASK(32) }
+  else if (C <= 52 && sc && xl && k <= kAssignXLK) { MW_AS(52, 64) }  // XL: 26 feature pairs, not 32
   else { MW_ASK(64) }
 #undef MW_ASK
 #undef MW_AS
