@@ -707,13 +707,13 @@ __global__ void __launch_bounds__(256) lloyd_pass_kernel(const float* __restrict
 // 256 VGPRs and an 8-byte spill).  Config-5 cohort fit (2 x 40k^2 x 50
 // slides, same box, profiles/r04/bench_c5x2_synth*.json): 476.3 -> 460.4 ms.
 // The default; MW_LLOYD_FIRST_W2=0 takes the unbounded instance (same bits)
-template <int KIND>
+template <int FMAX, int KIND>
 __global__ void __launch_bounds__(256, 2) lloyd_first_w2_kernel(const float* __restrict__ X, int64_t S, int F,
                                                                const float* __restrict__ ga,
                                                                const float* __restrict__ gb,
                                                                const int* __restrict__ qexp,
                                                                const LloydFitsArg fits, int n, int64_t R) {
-  lloyd_pass_body<64, 0, KIND, 1>(X, S, F, ga, gb, qexp, fits, n, R);
+  lloyd_pass_body<FMAX, 0, KIND, 1>(X, S, F, ga, gb, qexp, fits, n, R);
 }
 
 // kList, first launch: the bound test of every row of the block's range from
@@ -966,7 +966,11 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     MW_LAUNCH_CHECK();
     return MW_OK;
   }
-  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : 64;
+  // F in (32, 52]: 26 feature pairs instead of 32 in every distance (the 6
+  // more only add exact zeros: the same bits; MW_LLOYD_FM52=0 keeps 64, A/B)
+  const char* e52 = getenv("MW_LLOYD_FM52");
+  const bool fm52 = !(e52 && e52[0] == '0');
+  const int FM = F <= 8 ? 8 : F <= 16 ? 16 : F <= 32 ? 32 : (F <= 52 && fm52) ? 52 : 64;
   const dim3 grid((unsigned)G * (unsigned)n);
   // kFirst: fp64 accumulators for ceil(kmax / 16) label blocks x the feature
   // blocks, at most 4 (else the sums go through LDS atomics)
@@ -979,8 +983,10 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     const char* e = getenv("MW_LLOYD_FIRST_SUM");
     return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
-  if (mode == 0 && kind == kFirst && kmax <= 16 && (first_sum == 1 || (first_sum < 0 && FM == 64)))
+  if (mode == 0 && kind == kFirst && kmax <= 16 && (first_sum == 1 || (first_sum < 0 && FM >= 52)))
     kind = kFirstSum;
+  // FM = 52: the one-hot MFMA M-step takes 16-feature blocks (52 is not a multiple)
+  if (mode == 0 && kind == kFirst && FM == 52) kind = kmax <= 16 ? kFirstSum : kFirstAtomic;
   const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
   if (mode == 0 && kind == kList) {
     hipLaunchKernelGGL(lloyd_mark_kernel, grid, dim3(256), 0, s, fits, n, S, F, R);
@@ -1009,13 +1015,18 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   }();
   if (first_w2 && FM == 64 && mode == 0 && (kind == kFirst || kind == kFirstSum) && MBF == 1) {
     if (kind == kFirst)
-      hipLaunchKernelGGL(lloyd_first_w2_kernel<kFirst>, grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp, fits, n, R);
+      hipLaunchKernelGGL((lloyd_first_w2_kernel<64, kFirst>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp,
+                         fits, n, R);
     else
-      hipLaunchKernelGGL(lloyd_first_w2_kernel<kFirstSum>, grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp, fits, n,
-                         R);
+      hipLaunchKernelGGL((lloyd_first_w2_kernel<64, kFirstSum>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp,
+                         fits, n, R);
+  } else if (first_w2 && FM == 52 && mode == 0 && kind == kFirstSum) {
+    hipLaunchKernelGGL((lloyd_first_w2_kernel<52, kFirstSum>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp,
+                       fits, n, R);
   } else if (FM == 8) { MW_LPF(8) }
   else if (FM == 16) { MW_LPF(16) }
   else if (FM == 32) { MW_LPF(32) }
+  else if (FM == 52) { MW_LPF(52) }
   else { MW_LPF(64) }
 #undef MW_LPF
 #undef MW_LP

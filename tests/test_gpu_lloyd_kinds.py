@@ -119,3 +119,35 @@ def test_sweep_in_slide_order_equals_draw_order(gpu, monkeypatch):
         assert a[3] == b[3], f"k={k} inertia"
         np.testing.assert_array_equal(b[0], a[0], err_msg=f"k={k} labels")
         np.testing.assert_array_equal(b[1], a[1], err_msg=f"k={k} centers")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("C", [50, 45, 33])
+def test_fm52_instances_equal_fm64(gpu, monkeypatch, C):
+    """At 33 <= F <= 52 the Lloyd passes run the FMAX = 52 instances (26
+    feature pairs per distance; the first pass's M-step by label-sorted sums
+    or LDS atomics, never the 16-feature MFMA blocks): every fit bitwise the
+    FMAX = 64 instances' (MW_LLOYD_FM52=0) -- labels, centers, n_iter,
+    inertia -- for k = 8..20 batched and k = 8 alone through KMeans."""
+    from milwrm_amd import kmeans as KM
+
+    rows = _rows(C, 768)
+    ks = [8, 12, 17, 20]
+    out = {}
+    for fm in ("0", "1"):
+        monkeypatch.setenv("MW_LLOYD_FM52", fm)
+        with contextlib.redirect_stdout(sys.stderr):
+            fits = KM.fit_many(rows, ks, random_state=18)
+            one = KM.KMeans(n_clusters=8, random_state=18).fit(rows)
+        out[fm] = ([(np.asarray(m.labels_).copy(), m.cluster_centers_.copy(), m.n_iter_, m.inertia_)
+                    for m in fits], (np.asarray(one.labels_).copy(), one.cluster_centers_.copy(),
+                                     one.n_iter_, one.inertia_))
+    for (a, b), k in zip(zip(out["0"][0], out["1"][0]), ks):
+        assert a[2] == b[2], f"F={C} k={k}: n_iter {b[2]} vs {a[2]}"
+        np.testing.assert_array_equal(a[0], b[0], err_msg=f"F={C} k={k} labels")
+        np.testing.assert_array_equal(a[1], b[1], err_msg=f"F={C} k={k} centers")
+        assert a[3] == b[3]
+    a, b = out["0"][1], out["1"][1]
+    assert a[2] == b[2] and a[3] == b[3]
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
