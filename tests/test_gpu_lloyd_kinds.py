@@ -5,8 +5,10 @@ one batched launch, and repeated runs agree; so does the dense pass (the
 f16-split x . C^T of every fit on the matrix cores, exact recheck of near
 ties), every iteration or until fewer than 9 fits run (then bounded passes
 from recomputed bounds); at F = 30 (FMAX = 32) and at
-F = 50 / 45 (FMAX = 64: F-sized LDS tiles, masked tile stores with a zeroed
-pad, the kList gather into the smaller tile; odd F takes the scalar gather).
+F = 50 / 45 (FMAX = 52 instances: 26 feature pairs, 52-float tile rows with a
+zeroed pad; odd F takes the scalar gather).  test_fm52_instances_equal_fm64
+checks those against the FMAX = 64 instances (F-sized LDS tiles, masked tile
+stores, the kList gather into the smaller tile) bit for bit.
 The k-means++ passes at F > 32 (F-sized tiles, pipelined table loads) pick
 the oracle's indices on the same fp32 rows.  Regression: the queue pass
 gathers only the F floats of each row into LDS, and the scaled-row read
