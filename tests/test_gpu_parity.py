@@ -489,7 +489,8 @@ def _same_bits(a, b):
 
 @pytest.mark.parametrize("H,W,C,k,feats", [
     (300, 260, 30, 8, None), (130, 64, 30, 16, None), (190, 210, 30, 8, [3, 1, 4, 15, 9, 2, 6]),
-    (200, 200, 16, 8, None), (160, 96, 64, 12, None), (1031, 778, 30, 8, None)])
+    (200, 200, 16, 8, None), (160, 96, 64, 12, None), (1031, 778, 30, 8, None),
+    (150, 130, 50, 8, None), (120, 100, 45, 6, list(range(44, 4, -1)))])
 def test_fused_epilogues_match_materialised(gpu, H, W, C, k, feats):
     """Blur with the sample / assign epilogue (blurred slide never stored) is
     bit-identical to blur → gather and blur → assign: same X rows, column
