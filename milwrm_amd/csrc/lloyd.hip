@@ -716,6 +716,19 @@ __global__ void __launch_bounds__(256, 2) lloyd_first_w2_kernel(const float* __r
   lloyd_pass_body<FMAX, 0, KIND, 1>(X, S, F, ga, gb, qexp, fits, n, R);
 }
 
+// the first pass at 17..32 features under a three-waves-per-SIMD bound (the
+// unbounded instance holds 167 VGPRs + 16 AGPRs: two waves per SIMD; this one
+// 168 VGPRs, no AGPRs, no spill).  Opt-in (MW_LLOYD_FIRST_W3=1) until measured
+// against the unbounded instance (same bits)
+template <int FMAX, int KIND>
+__global__ void __launch_bounds__(256, 3) lloyd_first_w3_kernel(const float* __restrict__ X, int64_t S, int F,
+                                                               const float* __restrict__ ga,
+                                                               const float* __restrict__ gb,
+                                                               const int* __restrict__ qexp,
+                                                               const LloydFitsArg fits, int n, int64_t R) {
+  lloyd_pass_body<FMAX, 0, KIND, 1>(X, S, F, ga, gb, qexp, fits, n, R);
+}
+
 // kList, first launch: the bound test of every row of the block's range from
 // the row state alone (4 consecutive rows per lane, 4 groups of 256 rows per
 // wave in flight, no barrier until the end).  Decided rows get their drifted
@@ -1022,6 +1035,12 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
                          fits, n, R);
   } else if (first_w2 && FM == 52 && mode == 0 && kind == kFirstSum) {
     hipLaunchKernelGGL((lloyd_first_w2_kernel<52, kFirstSum>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp,
+                       fits, n, R);
+  } else if (FM == 32 && mode == 0 && kind == kFirst && MBF == 1 && [] {
+               const char* e = getenv("MW_LLOYD_FIRST_W3");
+               return e && e[0] == '1';
+             }()) {
+    hipLaunchKernelGGL((lloyd_first_w3_kernel<32, kFirst>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp,
                        fits, n, R);
   } else if (FM == 8) { MW_LPF(8) }
   else if (FM == 16) { MW_LPF(16) }

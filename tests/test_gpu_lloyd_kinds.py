@@ -153,3 +153,25 @@ def test_fm52_instances_equal_fm64(gpu, monkeypatch, C):
     assert a[2] == b[2] and a[3] == b[3]
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
+
+
+@pytest.mark.timeout(300)
+def test_first_pass_three_waves_equals_unbounded(gpu, monkeypatch):
+    """The first pass at F <= 32 under the three-waves-per-SIMD register bound
+    (lloyd_first_w3_kernel, MW_LLOYD_FIRST_W3=1) gives the unbounded
+    instance's fits bit for bit: labels, centers, n_iter, inertia."""
+    from milwrm_amd import kmeans as KM
+
+    rows = _rows(30, 1024)
+    out = {}
+    for w3 in ("0", "1"):
+        monkeypatch.setenv("MW_LLOYD_FIRST_W3", w3)
+        with contextlib.redirect_stdout(sys.stderr):
+            one = KM.KMeans(n_clusters=8, random_state=18).fit(rows)
+            fits = KM.fit_many(rows, [5, 8, 13], random_state=18)
+        out[w3] = [(np.asarray(m.labels_).copy(), m.cluster_centers_.copy(), m.n_iter_, m.inertia_)
+                   for m in [one] + list(fits)]
+    for a, b in zip(out["0"], out["1"]):
+        assert a[2] == b[2] and a[3] == b[3]
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
