@@ -718,8 +718,9 @@ __global__ void __launch_bounds__(256, 2) lloyd_first_w2_kernel(const float* __r
 
 // the first pass at 17..32 features under a three-waves-per-SIMD bound (the
 // unbounded instance holds 167 VGPRs + 16 AGPRs: two waves per SIMD; this one
-// 168 VGPRs, no AGPRs, no spill).  Opt-in (MW_LLOYD_FIRST_W3=1) until measured
-// against the unbounded instance (same bits)
+// 168 VGPRs, no AGPRs, no spill): 0.88-0.92 -> 0.83 ms per config-2 pass,
+// fit 7.43-7.45 -> 7.35-7.40 ms (profiles/r04/lloyd_w3_*).  The default;
+// MW_LLOYD_FIRST_W3=0 takes the unbounded instance (same bits)
 template <int FMAX, int KIND>
 __global__ void __launch_bounds__(256, 3) lloyd_first_w3_kernel(const float* __restrict__ X, int64_t S, int F,
                                                                const float* __restrict__ ga,
@@ -1038,7 +1039,7 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
                        fits, n, R);
   } else if (FM == 32 && mode == 0 && kind == kFirst && MBF == 1 && [] {
                const char* e = getenv("MW_LLOYD_FIRST_W3");
-               return e && e[0] == '1';
+               return !(e && e[0] == '0');
              }()) {
     hipLaunchKernelGGL((lloyd_first_w3_kernel<32, kFirst>), grid, dim3(256), lds, s, d_X, S, F, d_a, d_b, d_qexp,
                        fits, n, R);

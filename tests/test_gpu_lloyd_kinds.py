@@ -158,8 +158,9 @@ def test_fm52_instances_equal_fm64(gpu, monkeypatch, C):
 @pytest.mark.timeout(300)
 def test_first_pass_three_waves_equals_unbounded(gpu, monkeypatch):
     """The first pass at F <= 32 under the three-waves-per-SIMD register bound
-    (lloyd_first_w3_kernel, MW_LLOYD_FIRST_W3=1) gives the unbounded
-    instance's fits bit for bit: labels, centers, n_iter, inertia."""
+    (lloyd_first_w3_kernel, the default) gives the unbounded instance's
+    fits (MW_LLOYD_FIRST_W3=0) bit for bit: labels, centers, n_iter,
+    inertia."""
     from milwrm_amd import kmeans as KM
 
     rows = _rows(30, 1024)
