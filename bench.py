@@ -306,6 +306,37 @@ def design_point(H, W, C, k, comm, lab_hard, steps=3):
             "kmeans_fit_ms": round(fit.get("total_ms", 0.0) / steps, 4)}
 
 
+def host_outputs(lab):
+    """Cost of the reference-format outputs of one slide, outside the timed
+    step: ``tissue_IDs[0]`` and ``confidence_IDs[0]`` as float64 H x W host
+    arrays with NaN outside the mask (MILWRM.py:275-276, 444-445), converted
+    on first access from the device's int8 labels and fp32 confidences (one
+    page-locked D2H copy each, then a threaded host expansion)."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tid = lab.tissue_IDs[0]
+    t1 = time.perf_counter()
+    cid = lab.confidence_IDs[0]
+    t2 = time.perf_counter()
+    n = int(tid.size)
+    # the round-4 conversion (pageable .cpu(), single-threaded numpy astype /
+    # NaN fill; the confidences widened to fp64 on the device first), for comparison
+    t3 = time.perf_counter()
+    a = lab._labels_dev[0].cpu().numpy().astype(np.float64)
+    a[a < 0] = np.nan
+    b = lab._conf_dev[0].double().cpu().numpy()
+    t4 = time.perf_counter()
+    same = bool(np.array_equal(a, tid, equal_nan=True) and np.array_equal(b, cid, equal_nan=True))
+    del a, b
+    return {"pixels": n, "tissue_IDs_ms": round((t1 - t0) * 1e3, 3),
+            "confidence_IDs_ms": round((t2 - t1) * 1e3, 3),
+            "round4_conversion_ms": round((t4 - t3) * 1e3, 3), "equal_to_round4": same,
+            "d2h_bytes": 5 * n, "host_bytes_written": 16 * n,
+            "note": "first access of lab.tissue_IDs[0] / lab.confidence_IDs[0] (float64, NaN outside "
+                    "the mask) after the timed steps; not part of the headline step, whose outputs "
+                    "stay in HBM"}
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -461,6 +492,8 @@ def main():
         out["config"]["lloyd_iters"] = n_iter
         out["pipeline_roofline"] = {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,
                                     "unit": "GB/s", "frac": pipe_gbps / (HBM_PEAK_GBPS * world)}
+    if not args.sweep:
+        out["host_outputs"] = host_outputs(lab)
     if (world == 1 and not args.sweep and args.mode == "hard" and not args.no_design_point
             and source == "device" and n_sl == 1 and H * W * C * 2 <= 20e9):
         out["design_point"] = design_point(H, W, C, args.k, comm, lab)

@@ -434,6 +434,14 @@ int mw_synth_rows(int H, int W, int C, int y0, int y1, const float* d_seed_yx, i
                   const float* d_profiles, int n_domains, int shape_k, int bg_rows, uint64_t seed,
                   uint16_t* d_img, uint8_t* d_mask, void* stream);
 
+/* ---- reference-format label-pass outputs (host) ----------------------------
+ * tissue_IDs[i] / confidence_IDs[i] as the reference holds them: float64 H x W
+ * with NaN outside the mask (MILWRM.py:275-276, 444-445), from the compact
+ * device outputs copied to host memory (int8 labels, -1 = no domain; fp32
+ * confidences).  Host loops on `threads` threads (<= 1: the calling thread). */
+int mw_host_labels_f64(const int8_t* h_lab, int64_t n, double* h_out, int threads);
+int mw_host_f32_to_f64(const float* h_in, int64_t n, double* h_out, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,7 @@ import numpy as np
 import pandas as pd
 import torch
 
+from . import _native as N
 from . import device as D
 from .assign import (assign_image, assign_rows, banded_assign_image, blur_assign_image, dm_total,
                      domain_means, domain_sse_deferred, domain_sse_image, domain_sse_rows,
@@ -116,7 +117,7 @@ def estimate_confidence_score_mxif(image, use_path, scaler, centroids, features,
     if use_path:
         image = img.from_npz(image + ".npz")
     lab, conf, dom = _assign_img(image, features, centroids, scaler)
-    cid = conf.double().cpu().numpy()
+    cid = _conf_to_host(conf)
     tid = np.asarray(tissue_ID)
     own = _labels_to_host(lab)
     if tid.shape == own.shape and np.array_equal(np.nan_to_num(tid, nan=-1), np.nan_to_num(own, nan=-1)):
@@ -314,10 +315,28 @@ def _gather_deferred(image: img, feat, idx, r2p, X_out) -> bool:
                        truncate=truncate)
 
 
+def _host_threads() -> int:
+    """Threads of the host conversion loops (the box's CPU share is 16)."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def _d2h_pinned(t: torch.Tensor) -> torch.Tensor:
+    """One asynchronous copy of a device tensor into page-locked host memory
+    (torch's caching host allocator: the staging buffer is reused), then a
+    wait for it."""
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    torch.cuda.current_stream().synchronize()
+    return h
+
+
 def _labels_to_host(lab: torch.Tensor) -> np.ndarray:
-    a = lab.cpu().numpy().astype(np.float64)
-    a[a < 0] = np.nan
-    return a
+    """tissue_IDs[i] as the reference holds it (MILWRM.py:275-276): float64,
+    NaN outside the mask, from the device's int8 labels (-1 = no domain)."""
+    h = _d2h_pinned(lab)
+    out = np.empty(tuple(lab.shape), dtype=np.float64)
+    N.call("mw_host_labels_f64", h.data_ptr(), h.numel(), out.ctypes.data, _host_threads())
+    return out
 
 
 class _LazyHostList(list):
@@ -343,7 +362,12 @@ class _LazyHostList(list):
 
 
 def _conf_to_host(conf: torch.Tensor) -> np.ndarray:
-    return conf.double().cpu().numpy()
+    """confidence_IDs[i] (MILWRM.py:444-445): float64 from the device's fp32
+    confidences (NaN outside the mask stays NaN)."""
+    h = _d2h_pinned(conf)
+    out = np.empty(tuple(conf.shape), dtype=np.float64)
+    N.call("mw_host_f32_to_f64", h.data_ptr(), h.numel(), out.ctypes.data, _host_threads())
+    return out
 
 
 # ---------------------------------------------------------------- classes

@@ -113,15 +113,34 @@ class img:
 
         if self._dev is None:
             if self._host is None and self._src is not None:
-                self._dev = self._src.materialize()  # an explicit whole-slide read
+                src = self._src
+                self._fits_whole(src.H * src.row_bytes)
+                self._dev = src.materialize()  # an explicit whole-slide read
             else:
                 a = self._host if self._host.ndim > 2 else self._host[:, :, None]
-                RESIDENCY.admit(self, self._raw_nbytes())
+                if not RESIDENCY.admit(self, self._raw_nbytes()):
+                    self._fits_whole(self._raw_nbytes())  # over the budget: only if HBM holds it
                 self._dev = D.to_device_image(a)
             RESIDENCY.register(self, self._dev.numel() * self._dev.element_size())
         else:
             RESIDENCY.touch(self)
         return self._dev
+
+    def _fits_whole(self, nbytes: int):
+        """Raise a MemoryError naming the streamed alternative when a
+        whole-slide device copy of ``nbytes`` cannot be had even after evicting
+        every other resident slide (instead of an allocator failure deep in a
+        pass)."""
+        from .stream import RESIDENCY, alloc_bytes
+
+        RESIDENCY.release(nbytes + (256 << 20))
+        have = alloc_bytes()
+        if nbytes + (256 << 20) > have:
+            raise MemoryError(
+                f"this operation needs the whole raw slide in HBM ({nbytes / 2**30:.1f} GiB) and "
+                f"{have / 2**30:.1f} GiB can be allocated: the slide is streamed in row bands instead by "
+                f"the passes that take bands (calculate_non_zero_mean, log_normalize + blurring with the "
+                f"default batch mean, subsample_pixels, label_tissue_regions, confidence_score_images)")
 
     def _source(self):
         """None when the raw pixels are resident (or are admitted now: the

@@ -29,6 +29,8 @@ c_dp = C.POINTER(C.c_double)
 # name -> (restype, argtypes)
 _PROTOS = {
     "mw_version": (c_i32, []),
+    "mw_host_labels_f64": (c_i32, [c_vp, c_i64, c_vp, c_i32]),
+    "mw_host_f32_to_f64": (c_i32, [c_vp, c_i64, c_vp, c_i32]),
     "mw_last_error": (C.c_char_p, []),
     "mw_stream_blocks": (c_i32, [c_i64]),
     "mw_nz_stats_ws_bytes": (c_sz, [c_i64, c_i32]),

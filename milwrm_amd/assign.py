@@ -92,8 +92,9 @@ def blur_assign_image(raw, sigma: float, inv_mean, pseudoval: float, mu, inv,
 def _assign_band_rows(src, r, extra_per_row, band_rows):
     """Output rows per band of the banded label / QC passes: ``band_rows``,
     else ``MW_ASSIGN_BAND_ROWS``, else (resident slide) what half the free
-    HBM holds as fp32, (streamed slide) ``stream.band_rows_for``."""
-    from .stream import band_rows_for, free_bytes
+    HBM holds as fp32 (what one allocation can get: ``stream.alloc_bytes``),
+    (streamed slide) ``stream.band_rows_for``."""
+    from .stream import alloc_bytes, band_rows_for
 
     if band_rows is not None:
         return int(band_rows)
@@ -101,8 +102,21 @@ def _assign_band_rows(src, r, extra_per_row, band_rows):
     if env:
         return int(env)
     if src.zero_copy:
-        return int(free_bytes() // 2 // extra_per_row) - 2 * r
+        return int(alloc_bytes() // 2 // extra_per_row) - 2 * r
     return band_rows_for(src, extra_per_row)
+
+
+def _band_buffer(H, W, C, r, band_rows, min_band=16):
+    """The reused fp32 band buffer of the banded passes and the band height it
+    holds: ``band_rows`` output rows + 2r halo rows, lower if that one
+    allocation fails (``stream.alloc_rows`` halves it on an out-of-memory
+    error, down to ``min_band`` output rows)."""
+    from .stream import alloc_rows
+
+    want = min(H, band_rows + 2 * r)
+    buf = alloc_rows(want, (W, C), torch.float32, min_rows=min(want, min_band + 2 * r))
+    got = int(buf.shape[0])
+    return buf, (band_rows if got >= want else got - 2 * r)
 
 
 def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx, mu,
@@ -130,6 +144,11 @@ def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
     w = D.gaussian_taps(sigma, truncate)
     r = (len(w) - 1) // 2
     row_bytes = W * C * 4
+    from .stream import RESIDENCY
+
+    # the outputs (5 bytes per pixel) and a minimal band must fit: cached
+    # scratch of earlier passes and resident copies of other slides go first
+    RESIDENCY.release((r1 - r0) * W * 5 + (16 + 2 * r) * row_bytes + (256 << 20))
     band_rows = _assign_band_rows(src, r, row_bytes, band_rows)
     if band_rows < 16:
         return None
@@ -138,7 +157,7 @@ def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
     lab = torch.empty((r1 - r0, W), dtype=torch.int8, device=dev)
     conf = torch.empty((r1 - r0, W), dtype=torch.float32, device=dev)
     dom = torch.zeros(2 * k, dtype=torch.float64, device=dev)
-    buf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=dev)
+    buf, band_rows = _band_buffer(H, W, C, r, band_rows)
     for y0, y1, a, rb in bands(src, band_rows, r, r0, r1):
         out = buf[:rb.shape[0]]
         D.blur(rb, sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
@@ -339,7 +358,7 @@ def domain_sse_deferred(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
         band_rows = -(-H // ((1 << 10) - 1))
     dev = D.device()
     lab = _labels_i8(tissue_id, H * W, k, dev)
-    buf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=dev)
+    buf, band_rows = _band_buffer(H, W, C, r, band_rows)
 
     def bands():
         for y0, y1, a, rb in read_bands(src, band_rows, r):

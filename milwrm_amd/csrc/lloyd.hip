@@ -438,12 +438,12 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
     }
   } else if constexpr (MODE == 0 && KIND == kList) {
     // ============================ list pass =============================
-    // Two stages per wave: (A) the listed rows, 64 at a time: gather, the
-    // own-center distance tightens the upper bound, rows it decides are done;
-    // the rest go to a per-wave queue of rows that need every distance; (B)
-    // each full 64 of that queue (and the remainder at the end) runs the
-    // k-distance E-step with every lane busy.  The decisions are those of
-    // finish_rows (same tests, same arithmetic): same labels, same sums.
+    // One stage per wave: the listed rows 64 at a time (their row state
+    // loaded with the list entries, before the gather), then finish_rows on
+    // the batch: the own-center distance tightens the upper bound, and the
+    // rows it does not decide run the k-distance E-step in the same wave
+    // (lanes of decided rows idle).  The decisions are those of every other
+    // pass kind (same tests, same arithmetic): same labels, same sums.
     const int G = (int)(gridDim.x / n);
     const char* wsb = reinterpret_cast<const char*>(fit.ws);
     const size_t loff = lloyd_list_off(G, k, F);

@@ -47,9 +47,30 @@ class Workspace:
         b = self._bufs.get(key)
         nbytes = max(int(nbytes), 256)
         if b is None or b.numel() < nbytes:
-            b = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", dev))
+            self._bufs.pop(key, None)
+            b = None
+            try:
+                b = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", dev))
+            except torch.OutOfMemoryError:  # the other passes' cached scratch goes first
+                self.drop()
+                torch.cuda.empty_cache()
+                b = torch.empty(nbytes, dtype=torch.uint8, device=torch.device("cuda", dev))
             self._bufs[key] = b
         return b
+
+    def cached_bytes(self) -> int:
+        return sum(b.numel() for b in self._bufs.values())
+
+    def drop(self) -> int:
+        """Hand every cached scratch buffer back to the allocator (they are
+        made again on their next use; the kernels that used them were
+        enqueued on the current stream, so stream-ordered reuse is safe).
+        Returns the bytes dropped.  Config 5 at 4 slides per GPU: the fit's
+        workspace (~21 B per row, 21 GiB) and the sample map (8 B per pixel,
+        12 GiB) would otherwise stay cached through the label pass."""
+        n = self.cached_bytes()
+        self._bufs.clear()
+        return n
 
     def clear(self):
         self._bufs.clear()

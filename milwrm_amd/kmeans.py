@@ -291,17 +291,34 @@ def _exp_below(bound: float, bits: int = 40) -> int:
     return bits - int(np.frexp(bound)[1])
 
 
+def fit_memory_need(rows: DeviceRows, ks) -> int:
+    """HBM bytes the Lloyd fits of ``ks`` allocate (labels, bounds, workspaces)."""
+    S, F = rows.S, rows.F
+    return sum(S * 9 + lloyd_ws_bytes(S, k, F) for k in ks)
+
+
+def sort_memory_need(rows: DeviceRows) -> int:
+    """HBM bytes of ``fit_many``'s row sort beside the rows: the sorted copy
+    (S x F fp32), the int64 keys, the sort's values and indices (and its
+    temporaries, ~ one more int64 pair per row)."""
+    return rows.S * (rows.F * 4 + 8 + 16 + 16)
+
+
 def _check_fit_memory(rows: DeviceRows, ks) -> None:
     """HBM for the fits run in lockstep (per fit: uint8 labels + fp32 upper /
     lower bounds per row, 9 bytes, and its pass workspace), checked before
     any allocation so a too-large sweep raises with the remedy instead of
     failing inside torch (find_optimal_k runs 19 fits together)."""
-    S, F = rows.S, rows.F
     from .stream import RESIDENCY
 
-    need = sum(S * 9 + lloyd_ws_bytes(S, k, F) for k in ks)
+    need = fit_memory_need(rows, ks)
     free = RESIDENCY.release(need)  # resident copies of host-backed slides go first (stream.py)
+    if need > free and rows.draws:
+        rows.draws = None  # the rows' subsample draws (kept only for the sweep's row sort) go next
+        torch.cuda.empty_cache()
+        free = RESIDENCY.release(need)
     if need > free:
+        S = rows.S
         raise MemoryError(
             f"{len(ks)} k-means fits over {S} rows need {need / 2**30:.1f} GiB of HBM for their "
             f"labels, bounds and workspaces and {free / 2**30:.1f} GiB are free: shard the rows "
@@ -647,7 +664,14 @@ def fit_many(rows: DeviceRows, k_values, random_state=None, comm=None, **kw):
     # point: the M-step sums are exact integers and every other output is per
     # row, so the fits are bit for bit those over the draw order; labels go
     # back to draw order below)
-    perm = rows.spatial_order() if (SWEEP_SORT and len(models) > 1) else None
+    # (only when HBM holds the sorted copy and its sort beside the fits'
+    # state: otherwise the fits run over the draw order, the same bits)
+    perm = None
+    if SWEEP_SORT and len(models) > 1 and rows.draws:
+        from .stream import RESIDENCY
+        need = fit_memory_need(rows, [km.n_clusters for km in models]) + sort_memory_need(rows)
+        if RESIDENCY.release(need) >= need:
+            perm = rows.spatial_order()
     lrows = rows
     if perm is not None:
         lrows = DeviceRows(rows.X.index_select(0, perm), rows.mu, rows.inv, feature_var=rows._feature_var,

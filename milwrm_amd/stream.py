@@ -77,6 +77,40 @@ def free_bytes(dev=None) -> int:
     return int(free + st["reserved_bytes"]["all"]["current"] - st["allocated_bytes"]["all"]["current"])
 
 
+def alloc_bytes(dev=None) -> int:
+    """Bytes ONE new allocation can get: the device's free memory plus the
+    cached segments the allocator can hand back whole.  ``free_bytes`` also
+    counts the unused remainders of split segments (a segment partly in use
+    cannot be released), which no single large block can use: a 28.7 GiB band
+    buffer sized against 24.9 GiB free + 25.1 GiB of such cache failed."""
+    dev = torch.cuda.current_device() if dev is None else dev
+    free, _ = torch.cuda.mem_get_info(dev)
+    st = torch.cuda.memory.memory_stats_as_nested_dict(dev)
+    cached = st["reserved_bytes"]["all"]["current"] - st["allocated_bytes"]["all"]["current"]
+    split = st.get("inactive_split_bytes", {}).get("all", {}).get("current", 0)
+    return int(free + max(0, cached - split))
+
+
+def alloc_rows(rows: int, row_shape, dtype, min_rows: int = 1, dev=None) -> torch.Tensor:
+    """``torch.empty((rows, *row_shape))`` for a band buffer whose height is a
+    choice, not a requirement: on an allocation failure the cache is emptied
+    and the height halved (down to ``min_rows``, then the error propagates).
+    The caller reads the height it got from the tensor."""
+    dev = D.device() if dev is None else dev
+    rows = max(int(rows), int(min_rows), 1)
+    while True:
+        try:
+            return torch.empty((rows, *row_shape), dtype=dtype, device=dev)
+        except torch.OutOfMemoryError:
+            if D.WS.drop():  # the passes' cached scratch first, at the same height
+                torch.cuda.empty_cache()
+                continue
+            if rows <= min_rows:
+                raise
+            torch.cuda.empty_cache()
+            rows = max(int(min_rows), rows // 2)
+
+
 class Residency:
     """LRU of images whose raw pixels were uploaded whole from a host array
     (the only device copies that can be dropped and read again)."""
@@ -123,17 +157,21 @@ class Residency:
         while self.used() + nbytes > hbm_budget():
             if not self._evict_oldest(keep=im):
                 return False
-        while nbytes + (256 << 20) > free_bytes():
+        while nbytes + (256 << 20) > alloc_bytes():
             if not self._evict_oldest(keep=im):
                 return False
         return True
 
     def release(self, need: int) -> int:
-        """Evict until ``need`` bytes are free (or nothing is left to evict);
-        returns the free bytes."""
-        while free_bytes() < need and self._evict_oldest():
+        """Drop the passes' cached scratch (``device.WS``), then evict resident
+        slides, until ``need`` bytes can be allocated (``alloc_bytes``: free
+        memory plus the allocator's whole cached segments) or nothing is left
+        to free; returns those bytes."""
+        if alloc_bytes() < need and D.WS.drop():
+            torch.cuda.empty_cache()
+        while alloc_bytes() < need and self._evict_oldest():
             pass
-        return free_bytes()
+        return alloc_bytes()
 
 
 RESIDENCY = Residency()
@@ -350,18 +388,29 @@ def _side_stream(dev) -> torch.cuda.Stream:
     return s
 
 
+def _plan(H, band_rows, halo, r0, r1):
+    plan = []
+    for y0 in range(r0, r1, max(1, band_rows)):
+        y1 = min(r1, y0 + band_rows)
+        plan.append((y0, y1, max(0, y0 - halo), min(H, y1 + halo)))
+    return plan
+
+
 def bands(src: RowSource, band_rows: int, halo: int, r0: int = 0, r1=None):
     """Yield (y0, y1, a, raw): output rows [y0, y1) of [r0, r1) in bands of
     ``band_rows``, ``raw`` = the device rows [a, a + len(raw)) = [y0 - halo,
     y1 + halo) clipped to the slide.  A resident source yields views; any
     other is read into two buffers, band b+1 on a side stream while the
-    caller's work on band b runs on the current stream."""
+    caller's work on band b runs on the current stream.  When HBM cannot hold
+    two buffers of ``band_rows`` + 2 halo rows, the bands get lower
+    (``alloc_rows``); every output row is computed the same way whatever
+    band holds it.  The side stream's reads are ordered before the main
+    stream's later work also when the consumer stops early (an exception, or
+    a caller that abandons the generator), so the buffers are never handed
+    back to the allocator while a read into them is in flight."""
     H = src.H
     r1 = H if r1 is None else r1
-    plan = []
-    for y0 in range(r0, r1, max(1, band_rows)):
-        y1 = min(r1, y0 + band_rows)
-        plan.append((y0, y1, max(0, y0 - halo), min(H, y1 + halo)))
+    plan = _plan(H, band_rows, halo, r0, r1)
     if src.zero_copy:
         for y0, y1, a, b in plan:
             yield y0, y1, a, src.read(a, b, None)
@@ -372,7 +421,14 @@ def bands(src: RowSource, band_rows: int, halo: int, r0: int = 0, r1=None):
     rows = max(b - a for _, _, a, b in plan)
     nbuf = min(2, len(plan))
     RESIDENCY.release(nbuf * rows * src.row_bytes + (256 << 20))
-    bufs = [torch.empty((rows, src.W, src.C), dtype=src.dtype, device=dev) for _ in range(nbuf)]
+    lo = min(rows, 2 * halo + 1)
+    bufs = [alloc_rows(rows, (src.W, src.C), src.dtype, min_rows=lo, dev=dev)]
+    if nbuf > 1:
+        bufs.append(alloc_rows(int(bufs[0].shape[0]), (src.W, src.C), src.dtype, min_rows=lo, dev=dev))
+    got = min(int(b.shape[0]) for b in bufs)
+    if got < rows:  # HBM was short: lower bands into the buffers that could be had
+        plan = _plan(H, max(1, got - 2 * halo), halo, r0, r1)
+        nbuf = min(nbuf, len(plan))
     side = _side_stream(dev)
     main = torch.cuda.current_stream()
     ready = [None] * nbuf
@@ -391,17 +447,19 @@ def bands(src: RowSource, band_rows: int, halo: int, r0: int = 0, r1=None):
             ev.record(side)
         ready[s] = ev
 
-    issue(0)
-    for i, (y0, y1, a, b) in enumerate(plan):
-        if i + 1 < len(plan):
-            issue(i + 1)
-        s = i % nbuf
-        main.wait_event(ready[s])
-        yield y0, y1, a, bufs[s][:b - a]
-        ev = torch.cuda.Event()
-        ev.record(main)
-        free[s] = ev
-    main.wait_stream(side)
+    try:
+        issue(0)
+        for i, (y0, y1, a, b) in enumerate(plan):
+            if i + 1 < len(plan):
+                issue(i + 1)
+            s = i % nbuf
+            main.wait_event(ready[s])
+            yield y0, y1, a, bufs[s][:b - a]
+            ev = torch.cuda.Event()
+            ev.record(main)
+            free[s] = ev
+    finally:
+        main.wait_stream(side)
 
 
 def as_source(x) -> RowSource:
@@ -472,8 +530,9 @@ def blur_gather(src, sigma: float, inv_mean, pseudoval: float, feat: torch.Tenso
             if fused:
                 continue
         # the fused kernel does not take this shape: blur the band into fp32
-        if fbuf is None:
-            fbuf = torch.empty((min(H, band_rows + 2 * r), W, C), dtype=torch.float32, device=raw.device)
+        if fbuf is None:  # (bands no higher than the raw band just read)
+            fbuf = torch.empty((min(H, max(band_rows + 2 * r, hb)), W, C), dtype=torch.float32,
+                               device=raw.device)
         out = fbuf[:hb]
         D.blur(raw, sigma, inv_mean=inv_mean, pseudoval=pseudoval, out=out, truncate=truncate)
         core = out[y0 - a:y1 - a]
