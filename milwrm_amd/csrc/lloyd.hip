@@ -874,6 +874,7 @@ static int col_absmax_blocks(int64_t total, int F) {
 }  // namespace mw
 
 #include "lloyd_dense.h"
+#include "lloyd_dense2.h"
 
 using namespace mw;
 
@@ -966,6 +967,26 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     }();
     da.bscale = bscale;
     da.G = G;
+    // F <= 32: every fit in one block per row block (lloyd_dense2.h);
+    // MW_DENSE2=0 keeps the grouped form (A/B)
+    static const bool use2 = [] {
+      const char* e = getenv("MW_DENSE2");
+      return !(e && e[0] == '0');
+    }();
+    Dense2Arg d2{};
+    if (use2 && dense2_plan(h_fits, n, S, F, d2)) {
+      d2.bounds = da.bounds;
+      const size_t lds2 = dense2_lds_bytes(d2.coff[n], F);
+      if (lds2 <= 160 * 1024) {
+        hipLaunchKernelGGL(lloyd_dense2_kernel, dim3((unsigned)d2.G), dim3(64 * kD2Waves), lds2, s, d_X, S, F,
+                           d_a, d_b, d_qexp, fits, d2);
+        MW_LAUNCH_CHECK();
+        const int rlmax = lloyd_rec(kmax, F);
+        hipLaunchKernelGGL(lloyd_reduce_fits_kernel, dim3((rlmax + 31) / 32, n), dim3(256), 0, s, fits, d2.G, F);
+        MW_LAUNCH_CHECK();
+        return MW_OK;
+      }
+    }
     const dim3 gridd((unsigned)((G + 7) / 8 * 8) * (unsigned)da.ngroups);  // whole XCD rounds
     if (F <= 32) {
       hipLaunchKernelGGL(lloyd_dense_kernel<32>, gridd, dim3(256), dense_lds_bytes(32, F), s, d_X, S, F, d_a, d_b,

@@ -373,16 +373,18 @@ class _FitState:
 
 
 KIND_FIRST, KIND_TILE, KIND_QUEUE, KIND_LIST, KIND_DENSE = 0, 1, 2, 4, 5
-# the batched sweep's dense pass (lloyd_dense.h: x . C^T of every fit in the
-# launch on the matrix cores, exact fp32 recheck of near ties) while at least
-# this many fits run together; fewer -> the bounded passes.  Opt-in
-# (MW_LLOYD_DENSE=1): the k = 2..20 sweep at config 2 measured 0.91 s with it
-# against 0.70 s with the bounded passes (4.8 ms per dense launch over all
-# fits vs 2.6-2.9 ms per list launch)
+# the batched sweep's dense pass (lloyd_dense2.h at F <= 30: x . C^T of every
+# fit in the launch on the matrix cores, the norms folded into the two spare
+# features, keyed top two, exact fp32 recheck of near ties) while at least this
+# many fits run together; fewer -> the bounded passes.  Default at F <= 30
+# (round 5, config 4 sweep: 0.50 s against 0.65 s with the bounded passes;
+# DESIGN.md section 5); MW_LLOYD_DENSE=1 also takes F <= 64 (the grouped form,
+# lloyd_dense.h: slower than the bounded passes there), 0 turns it off
 DENSE_MIN_FITS = int(os.environ.get("MW_LLOYD_DENSE_MIN", "3"))
 # fit_many's Lloyd passes over the rows in slide order (DeviceRows.spatial_order)
 SWEEP_SORT = os.environ.get("MW_SWEEP_SORT", "1") != "0"
-USE_DENSE = os.environ.get("MW_LLOYD_DENSE", "0") == "1"
+DENSE_MODE = os.environ.get("MW_LLOYD_DENSE", "auto")
+USE_DENSE = DENSE_MODE != "0"
 # the few-undecided pass: kList (bound test and list in one launch, the listed
 # rows in a second) unless MW_LLOYD_LIST=0 (kQueue: both phases chunk by chunk
 # in one kernel)
@@ -528,7 +530,8 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
     if comm.sharded():
         S_glob = int(comm.all_gather_np(np.array([S], dtype=np.int64))[:, 0].sum())
 
-    dense_ok = USE_DENSE and F <= 64 and max(ks) <= 20  # lloyd_dense.h kDenseMaxFitK
+    # lloyd_dense2.h: F <= 30 (kD2MaxK 32); lloyd_dense.h: F <= 64, kDenseMaxFitK = 20
+    dense_ok = USE_DENSE and F <= (64 if DENSE_MODE == "1" else 30) and max(ks) <= 20
     for it in range(max_iter):
         active = [g for g in range(n) if not fits[g].done]
         if not active:

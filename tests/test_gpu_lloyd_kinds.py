@@ -62,6 +62,7 @@ def test_pass_kinds_equal_full_estep(gpu, monkeypatch, C, size):
         monkeypatch.setattr(KM, "QUEUE_BELOW", qb)
         monkeypatch.setattr(KM, "QUEUE_KIND", qk)
         monkeypatch.setattr(KM, "USE_DENSE", dmin is not None)
+        monkeypatch.setattr(KM, "DENSE_MODE", "1")  # F = 50 / 45: the grouped dense form too
         monkeypatch.setattr(KM, "DENSE_MIN_FITS", dmin or 1)
         if nobound:
             monkeypatch.setenv("MW_LLOYD_NOBOUND", "1")
@@ -77,6 +78,45 @@ def test_pass_kinds_equal_full_estep(gpu, monkeypatch, C, size):
             assert a[2] == b[2], f"k={k} {name}: n_iter {b[2]} vs {a[2]}"
             np.testing.assert_array_equal(b[0], a[0], err_msg=f"k={k} {name} labels")
             np.testing.assert_array_equal(b[1], a[1], err_msg=f"k={k} {name} centers")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("outlier", [300.0, 3000.0])
+def test_dense_keys_far_rows_equal_full_estep(gpu, monkeypatch, outlier):
+    """The dense pass's folded norms and keyed top two (lloyd_dense2.h) at
+    its edges: an odd number of fits with k = 1 and fits spanning two MFMA
+    tiles, rows whose |x|^2 passes kD2NormMax (their fits go to the exact
+    chain) and, at the larger outliers, centers past it too (the whole launch
+    on the exact chain).  Labels, centers and n_iter equal the plain E-step."""
+    import torch
+
+    from milwrm_amd import kmeans as KM
+
+    rng = np.random.default_rng(7)
+    S, F = 120_000, 30
+    cent = rng.normal(0.0, 6.0, size=(12, F))
+    X = cent[rng.integers(0, 12, size=S)] + rng.normal(0.0, 1.0, size=(S, F))
+    far = rng.choice(S, size=S // 100, replace=False)
+    X[far, :4] += rng.uniform(0.5, 1.0, size=(far.size, 4)) * outlier
+    rows = KM.DeviceRows.from_host(X.astype(np.float32))
+    ks = [1, 2, 3, 5, 9, 17, 20]
+    out = {}
+    for name, nobound, dense in [("full", True, False), ("dense", False, True)]:
+        monkeypatch.setattr(KM, "USE_DENSE", dense)
+        monkeypatch.setattr(KM, "DENSE_MIN_FITS", 1)
+        if nobound:
+            monkeypatch.setenv("MW_LLOYD_NOBOUND", "1")
+        else:
+            monkeypatch.delenv("MW_LLOYD_NOBOUND", raising=False)
+        with contextlib.redirect_stdout(sys.stderr):
+            fits = KM.fit_many(rows, ks, random_state=11)
+        out[name] = [(np.asarray(m.labels_).copy(), m.cluster_centers_.copy(), m.n_iter_) for m in fits]
+    torch.cuda.synchronize()
+    for i, k in enumerate(ks):
+        a, b = out["full"][i], out["dense"][i]
+        assert a[2] == b[2], f"k={k}: n_iter {b[2]} vs {a[2]}"
+        np.testing.assert_array_equal(b[0], a[0], err_msg=f"k={k} labels")
+        np.testing.assert_array_equal(b[1], a[1], err_msg=f"k={k} centers")
 
 
 @pytest.mark.timeout(300)
