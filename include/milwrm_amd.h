@@ -333,6 +333,38 @@ int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
                   uint8_t* d_labels, double* h_centers, double* h_inertia, int* h_n_iter,
                   int64_t* h_init_idx, void* d_ws, size_t ws_bytes, void* stream);
 
+/* ---- batched fits: the find_optimal_k sweep's Lloyd iterations ----------------
+ * Replaces kMeansRes' per-k `KMeans(n_clusters=k, random_state=seed).fit(X)`
+ * (MILWRM.py:29-54, called per k by find_optimal_k MILWRM.py:659-704) for n
+ * fits over the same rows, from given k x F scaled initial centers (h_init,
+ * the fits' blocks concatenated; the caller seeds them with mw_kpp_*): one
+ * iteration = one mw_lloyd_pass per pass kind for every fit still running,
+ * one record download; each fit returns exactly what mw_kmeans_fit returns
+ * for it alone (strict / tolerance convergence, tol absolute here,
+ * relocation, the extra E-step, inertia).  Rows as mw_lloyd_pass (d_a32,
+ * d_b32, d_qexp on the device; h_a32, h_b32, h_qexp, the column max |x|
+ * h_xmax[F] and the scaler h_mu / h_inv on the host).  Per fit g the caller
+ * owns d_labels[g] (S uint8, filled with 255), d_ub[g], d_lb[g] (S fp32) and
+ * d_ws[g] (mw_lloyd_ws_bytes); d_par: sum of (k F + 2k) fp32, d_out: sum of
+ * mw_lloyd_rec_len(k, F) fp64.  Pass-kind policy: first_kind (0 or 3),
+ * queue_kind (2 or 4) below queue_below of the rows recomputed, the dense pass
+ * while >= dense_min fits run (0: never), nobound != 0: no bound ever holds.
+ * Outputs: h_centers (the fits' k x F fp64 blocks), h_inertia[n],
+ * h_n_iter[n]; h_hist (may be NULL): per fit hist_cap x (changed, recomputed)
+ * int64, h_hist_len[n] entries; h_timing (may be NULL): 9 x (launches, ms,
+ * algorithmic bytes) of the passes by mode-0 kind 0..6, mode 1, mode 2.
+ * Synchronises `stream`. */
+int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_a32, const float* d_b32,
+                  const int32_t* d_qexp, const float* h_a32, const float* h_b32,
+                  const int32_t* h_qexp, const float* h_xmax, const double* h_mu,
+                  const double* h_inv, int n, const int* h_k, const double* h_init,
+                  uint8_t* const* d_labels, float* const* d_ub, float* const* d_lb,
+                  void* const* d_ws, float* d_par, double* d_out, int max_iter, double tol,
+                  int first_kind, int queue_kind, double queue_below, int dense_min,
+                  int nobound, double* h_centers, double* h_inertia, int* h_n_iter,
+                  int64_t* h_hist, int hist_cap, int* h_hist_len, double* h_timing,
+                  void* stream);
+
 /* ---- empty-cluster relocation support (_k_means_common.pyx:181-226) ---------
  * fp64 distance of every row to centers[labels]; returns the n largest
  * (value desc, index asc) into d_top_idx / d_top_val (n <= 64). */

@@ -70,6 +70,10 @@ _PROTOS = {
     "mw_kmeans_fit_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "mw_kmeans_fit": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_u32, c_i32,
                               C.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "mw_lloyd_fits": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                              c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, C.c_double,
+                              c_i32, c_i32, C.c_double, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp,
+                              c_vp, c_vp]),
     "mw_farthest_ws_bytes": (c_sz, [c_i64]),
     "mw_farthest": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_ws_bytes": (c_sz, [c_i64, c_i32]),

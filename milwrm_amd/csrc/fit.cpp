@@ -643,3 +643,430 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
   std::memcpy(h_centers, centers.data(), centers.size() * sizeof(double));
   return MW_OK;
 }
+
+// ---------------------------------------------------------------------------
+// mw_lloyd_fits: kmeans.py lloyd_fits (one process, no sharding) -- the
+// batched Lloyd iterations of several independent fits over the same rows,
+// host control flow step for step, so both front ends return the same bits.
+// Per iteration: one table upload, the passes grouped by kind (24 fits per
+// launch at most), one record download; the per-fit fp64 host arithmetic is
+// the one of mw_kmeans_fit above (numpy's reductions restated by np_sum).
+namespace mw {
+namespace {
+
+constexpr int kFitsMaxPerLaunch = 24;
+constexpr int kKindFirst = 0, kKindTile = 1, kKindDense = 5;
+
+struct FitsFit {
+  int k = 0;
+  std::vector<double> centers;
+  std::vector<float> prev32;
+  bool have_prev = false;
+  std::vector<int64_t> q_hi, q_lo, count;
+  bool done = false, strict = false, bounds_ok = true;
+  int n_iter = 0;
+  double drift_max = 0.0, prev_dmax = 0.0;  // float32 values (or inf), as the Python floats
+  int iexp = 0;
+  std::vector<int64_t> hist;  // (changed, recomputed) per pass
+};
+
+// kmeans.py _bound_tables + upload: the fp32 centers | drift | half
+// separation of one fit into `h` (k*F + 2k floats)
+void fits_tables(FitsFit& fs, int F, bool nobound, float* h) {
+  const int k = fs.k;
+  for (size_t i = 0; i < (size_t)k * F; ++i) h[i] = (float)fs.centers[i];
+  const float inf = std::numeric_limits<float>::infinity();
+  std::vector<float> drift32(k), half32(k);
+  double dmax;
+  if (nobound) {
+    for (int j = 0; j < k; ++j) drift32[j] = inf, half32[j] = 0.f;
+    dmax = std::numeric_limits<double>::infinity();
+  } else {
+    std::vector<double> tmp(F);
+    for (int j = 0; j < k; ++j) {
+      double drift = 0.0;
+      if (fs.have_prev) {
+        for (int f = 0; f < F; ++f) {
+          const double d = (double)h[(size_t)j * F + f] - (double)fs.prev32[(size_t)j * F + f];
+          tmp[f] = d * d;
+        }
+        drift = std::sqrt(np_sum(tmp.data(), F));
+      }
+      double half = std::numeric_limits<double>::infinity();
+      if (k > 1) {
+        double m = std::numeric_limits<double>::infinity();
+        for (int i = 0; i < k; ++i) {
+          if (i == j) continue;
+          for (int f = 0; f < F; ++f) {
+            const double d = (double)h[(size_t)j * F + f] - (double)h[(size_t)i * F + f];
+            tmp[f] = d * d;
+          }
+          m = std::min(m, np_sum(tmp.data(), F));
+        }
+        half = 0.5 * std::sqrt(m);
+      }
+      drift32[j] = round_f32(drift, true);
+      half32[j] = round_f32(half, false);
+    }
+    float m = drift32[0];
+    for (int j = 1; j < k; ++j) m = std::max(m, drift32[j]);
+    dmax = (double)m;
+  }
+  if (!fs.bounds_ok) {  // after dense passes: every row recomputed, bounds rewritten
+    for (int j = 0; j < k; ++j) drift32[j] = inf;
+    dmax = std::numeric_limits<double>::infinity();
+  }
+  fs.prev_dmax = fs.have_prev ? fs.drift_max : 0.0;
+  fs.prev32.assign(h, h + (size_t)k * F);
+  fs.have_prev = true;
+  fs.drift_max = dmax;
+  for (int j = 0; j < k; ++j) {
+    h[(size_t)k * F + j] = drift32[j];
+    h[(size_t)k * F + k + j] = half32[j];
+  }
+}
+
+}  // namespace
+}  // namespace mw
+
+extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_a32, const float* d_b32,
+                             const int32_t* d_qexp, const float* h_a32, const float* h_b32,
+                             const int32_t* h_qexp, const float* h_xmax, const double* h_mu,
+                             const double* h_inv, int n, const int* h_k, const double* h_init,
+                             uint8_t* const* d_labels, float* const* d_ub, float* const* d_lb,
+                             void* const* d_ws, float* d_par, double* d_out, int max_iter, double tol,
+                             int first_kind, int queue_kind, double queue_below, int dense_min,
+                             int nobound, double* h_centers, double* h_inertia, int* h_n_iter,
+                             int64_t* h_hist, int hist_cap, int* h_hist_len, double* h_timing,
+                             void* stream) {
+  MW_CHECK_ARG(d_X && d_a32 && d_b32 && d_qexp && h_a32 && h_b32 && h_qexp && h_xmax && h_mu && h_inv &&
+                   h_k && h_init && d_labels && d_ub && d_lb && d_ws && d_par && d_out && h_centers &&
+                   h_inertia && h_n_iter,
+               "mw_lloyd_fits: null pointer");
+  MW_CHECK_ARG(n >= 1 && F >= 1 && F <= 64 && S >= 1 && max_iter >= 1 && tol >= 0.0,
+               "mw_lloyd_fits: bad n / F / S / max_iter / tol");
+  hipStream_t st = as_stream(stream);
+  std::vector<FitsFit> fits(n);
+  std::vector<int64_t> poff(n + 1, 0), roff(n + 1, 0);
+  size_t coff = 0;
+  for (int g = 0; g < n; ++g) {
+    const int k = h_k[g];
+    MW_CHECK_ARG(k >= 1 && k <= 64 && S >= k, "mw_lloyd_fits: fit %d: k=%d", g, k);
+    FitsFit& fs = fits[g];
+    fs.k = k;
+    fs.centers.assign(h_init + coff, h_init + coff + (size_t)k * F);
+    coff += (size_t)k * F;
+    fs.q_hi.assign((size_t)k * F, 0);
+    fs.q_lo.assign((size_t)k * F, 0);
+    fs.count.assign(k, 0);
+    poff[g + 1] = poff[g] + (int64_t)k * F + 2 * k;
+    roff[g + 1] = roff[g] + mw_lloyd_rec_len(k, F);
+  }
+  std::vector<double> a64(F), b64(F), qscale(F);
+  for (int f = 0; f < F; ++f) {
+    a64[f] = (double)h_a32[f];
+    b64[f] = (double)h_b32[f];
+    qscale[f] = std::ldexp(1.0, -h_qexp[f]);
+  }
+  int kmax = 1;
+  for (int g = 0; g < n; ++g) kmax = std::max(kmax, h_k[g]);
+  const bool dense_ok = dense_min > 0 && kmax <= 20;  // (the caller checks F)
+
+  // host staging: pinned when the tables / records fit its regions
+  char* pin = pinned_staging();
+  const size_t par_bytes = (size_t)poff[n] * 4, rec_bytes = (size_t)roff[n] * 8;
+  std::vector<float> host_par_v;
+  std::vector<double> rec_v;
+  float* host_par;
+  double* rec;
+  const bool pin_par = pin && par_bytes <= kPinRec - kPinTab;
+  const bool pin_rec = pin && rec_bytes <= kPinRows - kPinRec;
+  if (pin_par) {
+    host_par = reinterpret_cast<float*>(pin + kPinTab);
+  } else {
+    host_par_v.assign(poff[n], 0.f);
+    host_par = host_par_v.data();
+  }
+  std::memset(host_par, 0, par_bytes);
+  if (pin_rec) {
+    rec = reinterpret_cast<double*>(pin + kPinRec);
+  } else {
+    rec_v.assign(roff[n], 0.0);
+    rec = rec_v.data();
+  }
+
+  // per-launch timing (bench.py's profiling): slot = kind (mode 0) or 6 + mode
+  struct Timed {
+    hipEvent_t a, b;
+    int slot;
+    double bytes;
+  };
+  std::vector<Timed> timed;
+  auto ev_fail = [&]() {
+    for (Timed& t : timed) {
+      (void)hipEventDestroy(t.a);
+      (void)hipEventDestroy(t.b);
+    }
+  };
+
+  auto upload = [&](const std::vector<int>& sel) -> int {
+    for (int g : sel) fits_tables(fits[g], F, nobound != 0, host_par + poff[g]);
+    MW_HIP(hipMemcpyAsync(d_par, host_par, par_bytes, hipMemcpyHostToDevice, st));
+    if (!pin_par) MW_HIP(hipStreamSynchronize(st));
+    return MW_OK;
+  };
+  auto launch = [&](const std::vector<int>& gs, int mode, int kind) -> int {
+    for (size_t i0 = 0; i0 < gs.size(); i0 += kFitsMaxPerLaunch) {
+      const size_t i1 = std::min(gs.size(), i0 + kFitsMaxPerLaunch);
+      std::vector<mw_lloyd_fit> arr(i1 - i0);
+      double nbytes = 0.0;
+      for (size_t i = i0; i < i1; ++i) {
+        const int g = gs[i];
+        const FitsFit& fs = fits[g];
+        mw_lloyd_fit& f = arr[i - i0];
+        float* base = d_par + poff[g];
+        f.centers = base;
+        f.drift = base + (size_t)fs.k * F;
+        f.half_sep = base + (size_t)fs.k * F + fs.k;
+        f.labels = d_labels[g];
+        f.ub = d_ub[g];
+        f.lb = d_lb[g];
+        f.ws = d_ws[g];
+        f.out = d_out + roff[g];
+        f.k = fs.k;
+        f.drift_max = (float)fs.drift_max;
+        f.inertia_exp = fs.iexp;
+        if (kind == kKindDense && mode == 0)  // rows once per launch, labels per fit
+          nbytes += 2.0 * S + (i == i0 ? (double)S * F * 4 : 0.0);
+        else
+          nbytes += 9.0 * S + ((mode || (kind != 2 && kind != 4)) ? (double)S * F * 4 : 0.0);
+      }
+      Timed t{};
+      if (h_timing) {
+        MW_HIP(hipEventCreate(&t.a));
+        MW_HIP(hipEventCreate(&t.b));
+        t.slot = mode ? 6 + mode : kind;
+        t.bytes = nbytes;
+        timed.push_back(t);
+        MW_HIP(hipEventRecord(t.a, st));
+      }
+      MW_TRY(mw_lloyd_pass(d_X, S, F, d_a32, d_b32, d_qexp, (int)arr.size(), arr.data(), mode, kind, st));
+      if (h_timing) MW_HIP(hipEventRecord(t.b, st));
+    }
+    return MW_OK;
+  };
+  auto download = [&]() -> int {
+    MW_HIP(hipMemcpyAsync(rec, d_out, rec_bytes, hipMemcpyDeviceToHost, st));
+    MW_HIP(hipStreamSynchronize(st));
+    return MW_OK;
+  };
+
+  // relocation scratch (allocated on the first empty cluster)
+  DevBuf far_buf;
+  size_t far_ws = 0;
+  double* d_c64 = nullptr;
+  int64_t* d_topi = nullptr;
+  double* d_topv = nullptr;
+  void* d_farws = nullptr;
+
+  int rc = MW_OK;
+  std::vector<double> cnew, weight, tmp(std::max(F, kmax));
+  for (int it = 0; it < max_iter && rc == MW_OK; ++it) {
+    std::vector<int> active;
+    for (int g = 0; g < n; ++g)
+      if (!fits[g].done) active.push_back(g);
+    if (active.empty()) break;
+    const bool dense_now = dense_ok && it > 0 && (int)active.size() >= dense_min;
+    if ((rc = upload(active)) != MW_OK) break;
+    // kind_of (kmeans.py): first pass, dense, else kTile / the few-undecided kind
+    std::vector<int> by_kind[8];
+    for (int g : active) {
+      const FitsFit& fs = fits[g];
+      int kind;
+      if (fs.hist.empty()) {
+        kind = first_kind;
+      } else if (dense_now) {
+        kind = kKindDense;
+      } else if (!fs.bounds_ok) {
+        kind = kKindTile;
+      } else {
+        double frac = (double)fs.hist.back() / (double)std::max<int64_t>(S, 1);
+        if (fs.prev_dmax > 0 && std::isfinite(fs.drift_max)) frac *= std::min(1.0, fs.drift_max / fs.prev_dmax);
+        kind = frac > queue_below ? kKindTile : queue_kind;
+      }
+      by_kind[kind].push_back(g);
+    }
+    for (int kind = 0; kind < 8 && rc == MW_OK; ++kind)
+      if (!by_kind[kind].empty()) rc = launch(by_kind[kind], 0, kind);
+    if (rc != MW_OK || (rc = download()) != MW_OK) break;
+    for (int g : active) {
+      FitsFit& fs = fits[g];
+      const int k = fs.k;
+      if (it > 0) fs.bounds_ok = !dense_now;
+      const double* r = rec + roff[g];
+      for (size_t i = 0; i < (size_t)k * F; ++i) {
+        fs.q_hi[i] += (int64_t)r[i];
+        fs.q_lo[i] += (int64_t)r[(size_t)k * F + i];
+        const int64_t carry = fs.q_lo[i] >> 32;
+        fs.q_hi[i] += carry;
+        fs.q_lo[i] -= carry << 32;
+      }
+      for (int j = 0; j < k; ++j) fs.count[j] += (int64_t)r[2 * (size_t)k * F + j];
+      const double* tail = r + 2 * (size_t)k * F + k;
+      const int64_t changed = (int64_t)tail[0];
+      fs.hist.push_back(changed);
+      fs.hist.push_back((int64_t)tail[1]);
+      cnew.assign((size_t)k * F, 0.0);
+      weight.assign(k, 0.0);
+      for (int j = 0; j < k; ++j) {
+        weight[j] = (double)fs.count[j];
+        for (int f = 0; f < F; ++f) {
+          const size_t i = (size_t)j * F + f;
+          const double sx = ((double)fs.q_hi[i] * 4294967296.0 + (double)fs.q_lo[i]) * qscale[f];
+          cnew[i] = a64[f] * sx + b64[f] * weight[j];
+        }
+      }
+      // empty-cluster relocation (_k_means_common.pyx:181-226)
+      std::vector<int> empty;
+      for (int j = 0; j < k; ++j)
+        if (weight[j] == 0.0) empty.push_back(j);
+      if (!empty.empty()) {
+        const int ne = (int)empty.size();
+        if (!far_buf.p) {
+          far_ws = fal(mw_farthest_ws_bytes(S));
+          if ((rc = dev_alloc<char>(far_buf, far_ws + fal(64 * 64 * 8) + 64 * 16)) != MW_OK) break;
+          d_farws = far_buf.p;
+          d_c64 = reinterpret_cast<double*>(static_cast<char*>(far_buf.p) + far_ws);
+          d_topi = reinterpret_cast<int64_t*>(static_cast<char*>(far_buf.p) + far_ws + fal(64 * 64 * 8));
+          d_topv = reinterpret_cast<double*>(d_topi + 64);
+        }
+        MW_HIP(hipMemcpyAsync(d_c64, fs.centers.data(), fs.centers.size() * 8, hipMemcpyHostToDevice, st));
+        if ((rc = mw_farthest(d_X, S, F, d_a32, d_b32, d_c64, k, d_labels[g], ne, d_topi, d_topv, d_farws,
+                              st)) != MW_OK)
+          break;
+        std::vector<int64_t> far_i(ne);
+        std::vector<double> far_v(ne);
+        MW_HIP(hipMemcpyAsync(far_i.data(), d_topi, ne * 8, hipMemcpyDeviceToHost, st));
+        MW_HIP(hipMemcpyAsync(far_v.data(), d_topv, ne * 8, hipMemcpyDeviceToHost, st));
+        MW_HIP(hipStreamSynchronize(st));
+        double vmax = far_v[0];
+        for (double v : far_v) vmax = std::max(vmax, v);
+        if (vmax != 0.0) {
+          std::vector<float> xr((size_t)ne * F);
+          std::vector<uint8_t> olds(ne);
+          for (int e = 0; e < ne; ++e) {
+            MW_HIP(hipMemcpyAsync(xr.data() + (size_t)e * F, d_X + far_i[e] * F, F * sizeof(float),
+                                  hipMemcpyDeviceToHost, st));
+            MW_HIP(hipMemcpyAsync(&olds[e], d_labels[g] + far_i[e], 1, hipMemcpyDeviceToHost, st));
+          }
+          MW_HIP(hipStreamSynchronize(st));
+          for (int e = 0; e < ne; ++e) {
+            const uint8_t old = olds[e];
+            for (int f = 0; f < F; ++f) {
+              const double x = ((double)xr[(size_t)e * F + f] - h_mu[f]) * h_inv[f];
+              cnew[(size_t)old * F + f] -= x;
+              cnew[(size_t)empty[e] * F + f] = x;
+            }
+            weight[empty[e]] = 1.0;
+            weight[old] -= 1.0;
+          }
+        }
+      }
+      // _average_centers (_k_means_common.pyx:229-258)
+      int amax = 0;
+      for (int j = 1; j < k; ++j)
+        if (weight[j] > weight[amax]) amax = j;
+      for (int j = 0; j < k; ++j) {
+        if (weight[j] > 0.0) {
+          const double rr = 1.0 / weight[j];
+          for (int f = 0; f < F; ++f) cnew[(size_t)j * F + f] *= rr;
+        } else {
+          for (int f = 0; f < F; ++f) cnew[(size_t)j * F + f] = cnew[(size_t)amax * F + f];
+        }
+      }
+      std::vector<double> shift2(k);
+      for (int j = 0; j < k; ++j) {
+        for (int f = 0; f < F; ++f) {
+          const double d = cnew[(size_t)j * F + f] - fs.centers[(size_t)j * F + f];
+          tmp[f] = d * d;
+        }
+        const double sh = std::sqrt(np_sum(tmp.data(), F));
+        shift2[j] = sh * sh;
+      }
+      fs.centers.swap(cnew);
+      fs.n_iter = it + 1;
+      if (changed == 0) {
+        fs.strict = fs.done = true;
+      } else if (np_sum(shift2.data(), k) <= tol) {
+        fs.done = true;
+      }
+      if (fs.done) MW_HIP(hipMemsetAsync(d_out + roff[g], 0, (size_t)(roff[g + 1] - roff[g]) * 8, st));
+    }
+  }
+  if (rc != MW_OK) {
+    ev_fail();
+    return rc;
+  }
+  for (FitsFit& fs : fits)
+    if (!fs.done) fs.n_iter = max_iter;
+
+  // final pass: the extra E-step when not strictly converged, and inertia
+  std::vector<double> xs2(F);
+  for (int f = 0; f < F; ++f) {
+    const double v = std::fabs(a64[f]) * (double)h_xmax[f] + std::fabs(b64[f]);
+    xs2[f] = v * v;
+  }
+  const double xnorm = std::sqrt(np_sum(xs2.data(), F));
+  std::vector<int> all(n);
+  for (int g = 0; g < n; ++g) {
+    all[g] = g;
+    FitsFit& fs = fits[g];
+    double cmax = 0.0;
+    for (int j = 0; j < fs.k; ++j) {
+      for (int f = 0; f < F; ++f) tmp[f] = fs.centers[(size_t)j * F + f] * fs.centers[(size_t)j * F + f];
+      const double v = std::sqrt(np_sum(tmp.data(), F));
+      cmax = j == 0 ? v : std::max(cmax, v);
+    }
+    const double xc = xnorm + cmax;
+    fs.iexp = exp_below(xc * xc * 1.01);
+  }
+  if ((rc = upload(all)) == MW_OK) {
+    for (int mode = 1; mode <= 2 && rc == MW_OK; ++mode) {
+      std::vector<int> sel;
+      for (int g = 0; g < n; ++g)
+        if ((fits[g].strict ? 2 : 1) == mode) sel.push_back(g);
+      if (!sel.empty()) rc = launch(sel, mode, kKindFirst);
+    }
+  }
+  if (rc == MW_OK) rc = download();
+  if (rc != MW_OK) {
+    ev_fail();
+    return rc;
+  }
+  size_t c = 0;
+  for (int g = 0; g < n; ++g) {
+    const FitsFit& fs = fits[g];
+    const double* tail = rec + roff[g + 1] - 4;
+    h_inertia[g] = (tail[2] * 4294967296.0 + tail[3]) * std::ldexp(1.0, -fs.iexp);
+    h_n_iter[g] = fs.n_iter;
+    std::memcpy(h_centers + c, fs.centers.data(), fs.centers.size() * sizeof(double));
+    c += fs.centers.size();
+    if (h_hist && h_hist_len) {
+      const int m = (int)std::min<size_t>(fs.hist.size() / 2, (size_t)hist_cap);
+      std::memcpy(h_hist + (size_t)g * hist_cap * 2, fs.hist.data(), (size_t)m * 2 * sizeof(int64_t));
+      h_hist_len[g] = m;
+    }
+  }
+  if (h_timing) {  // [slot][count, ms, bytes], slots 0..8
+    for (int i = 0; i < 27; ++i) h_timing[i] = 0.0;
+    for (Timed& t : timed) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, t.a, t.b);
+      h_timing[3 * t.slot] += 1.0;
+      h_timing[3 * t.slot + 1] += ms;
+      h_timing[3 * t.slot + 2] += t.bytes;
+    }
+  }
+  ev_fail();  // (destroys the events)
+  return MW_OK;
+}

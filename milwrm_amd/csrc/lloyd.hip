@@ -976,9 +976,14 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     Dense2Arg d2{};
     if (use2 && dense2_plan(h_fits, n, S, F, d2)) {
       d2.bounds = da.bounds;
-      const size_t lds2 = dense2_lds_bytes(d2.coff[n], F);
+      int waves = kD2Waves;  // 3 waves per SIMD, or 2 when the LDS of the launch needs it
+      size_t lds2 = dense2_lds_bytes(d2.coff[n], F, d2.ntile, waves);
+      if (lds2 > 160 * 1024) {
+        waves = 8;
+        lds2 = dense2_lds_bytes(d2.coff[n], F, d2.ntile, waves);
+      }
       if (lds2 <= 160 * 1024) {
-        hipLaunchKernelGGL(lloyd_dense2_kernel, dim3((unsigned)d2.G), dim3(64 * kD2Waves), lds2, s, d_X, S, F,
+        hipLaunchKernelGGL(lloyd_dense2_kernel, dim3((unsigned)d2.G), dim3(64 * waves), lds2, s, d_X, S, F,
                            d_a, d_b, d_qexp, fits, d2);
         MW_LAUNCH_CHECK();
         const int rlmax = lloyd_rec(kmax, F);

@@ -31,12 +31,19 @@
 // its own (kD2Blocks row blocks), reduced by lloyd_reduce_fits_kernel.
 #pragma once
 
+// timing variants (tools/probe/d2_variants.sh; wrong results): 1 = no closes,
+// 2 = no key updates, 3 = no queue flushes
+#ifndef MW_D2_VARIANT
+#define MW_D2_VARIANT 0
+#endif
+
 namespace mw {
 
 constexpr int kD2Tiles = 10;                // MFMA tiles of 32 center slots
 constexpr int kD2Slots = 32 * kD2Tiles;     // 8-aligned center slots of all fits
 constexpr int kD2Groups = kD2Slots / 8;     // 8-slot groups (one fit each)
-constexpr int kD2Waves = 8;                 // waves per block (one block per CU)
+constexpr int kD2Waves = 12;                // waves per block at most (one block per CU:
+                                            // 3 per SIMD; 8 when the LDS of the launch needs it)
 constexpr int kD2MaxBlocks = 512;           // row blocks (records per fit)
 // x' and c are split into f16 hi + lo (v = hi + lo to 2^-22); x . c =
 // hi.hi + lo.hi + hi.lo on the matrix cores (lo.lo, ~2^-22, dropped).
@@ -70,18 +77,16 @@ struct Dense2Arg {
   int64_t R;               // rows per row block (multiple of 32)
 };
 
-__host__ __device__ inline size_t d2_acc_off() {
+__host__ __device__ inline size_t d2_acc_off(int ntile) {
   return 3 * 32 * 4 + kD2Groups * 4 + 4 * (kMaxFits + 1) * 4 + 4 * kMaxFits * 8 + kD2Slots * 4 +
-         (size_t)kD2Tiles * 4 * 1024;
+         (size_t)ntile * 4 * 1024;
 }
-__host__ __device__ inline size_t d2_wave_bytes(int F) {
-  return kMaxFits * 32 + 2 * 64 * 4 + 128 * 4 + 16 + (((size_t)32 * F * 4 + 15) & ~(size_t)15);
-}
-__host__ __device__ inline size_t dense2_lds_bytes(int ksum, int F) {
-  size_t b = d2_acc_off();                                      // scaler, tables, |c|^2, A operands
+__host__ __device__ inline size_t d2_wave_bytes() { return kMaxFits * 32 + 2 * 64 * 4 + 128 * 4 + 16; }
+__host__ __device__ inline size_t dense2_lds_bytes(int ksum, int F, int ntile, int waves) {
+  size_t b = d2_acc_off(ntile);                                 // scaler, tables, |c|^2, A operands
   b += ((size_t)ksum * F * 8 + 15) & ~(size_t)15;               // cluster sums (int64)
   b += ((size_t)ksum * 4 + 2 * kMaxFits * 4 + 15) & ~(size_t)15;  // size deltas, changed, recomputed
-  b += (size_t)kD2Waves * d2_wave_bytes(F);                      // per wave: labels, queues, rows
+  b += (size_t)waves * d2_wave_bytes();                         // per wave: labels, queues
   return b;
 }
 
@@ -119,6 +124,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int nw = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6));  // waves of the block
   const int blk = blockIdx.x;
   const int nf = da.nf, ntile = da.ntile, ksum = da.coff[nf];
   char* sp = smem;
@@ -142,19 +148,17 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   float* s_cc = reinterpret_cast<float*>(sp);  // |c|^2 per slot (+inf: no center)
   sp += kD2Slots * 4;
   char* s_A = sp;  // [tile][kstep][hi, lo][lane][8 halves]
-  sp += (size_t)kD2Tiles * 4 * 1024;
+  sp += (size_t)ntile * 4 * 1024;
   unsigned long long* s_acc = reinterpret_cast<unsigned long long*>(sp);
   sp += ((size_t)ksum * F * 8 + 15) & ~(size_t)15;
   int* s_cnt = reinterpret_cast<int*>(sp);
   int* s_chg = s_cnt + ksum;
   int* s_rec = s_chg + kMaxFits;
   sp += ((size_t)ksum * 4 + 2 * kMaxFits * 4 + 15) & ~(size_t)15;
-  char* wp = sp + (size_t)wid * d2_wave_bytes(F);
+  char* wp = sp + (size_t)wid * d2_wave_bytes();
   uint8_t* w_lab = reinterpret_cast<uint8_t*>(wp);            // [fit][32 rows] old labels
   int* w_rq = reinterpret_cast<int*>(wp + kMaxFits * 32);      // recheck queue: row | fit << 8
   int* w_mq = w_rq + 2 * 64;                                   // M-step queue: row | fit << 8 | lab << 16 | old << 24
-  int* w_n = w_mq + 128;                                       // (pad)
-  float* w_rows = reinterpret_cast<float*>(w_n + 4);            // [32][F] the chunk's raw rows
 
   // ---- block setup: scaler, fit tables, |c|^2, A operands, zeroed sums ----
   for (int f = t; f < 32; f += blockDim.x) {
@@ -246,12 +250,17 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   const int nchunk = hi > lo ? (int)((hi - lo + 31) / 32) : 0;
   const int r = lane & 31, h = lane >> 5;
 
-  // ---- queues (rows of the current chunk: w_rows, F floats each); the
+  // ---- queues (rows of the current chunk, re-read from X: L2 hits); the
   // queue lengths are wave-uniform and live in scalar registers ----
   int nq_r = 0, nq_m = 0;
   // M-step of the queued changed (row, fit) pairs: two pairs per wave round,
   // lane = feature; four rounds' reads issued before their atomics
-  auto flush_m = [&]() {
+  int sink = 0;
+  auto flush_m = [&](int64_t r0) {
+    if (MW_D2_VARIANT == 3) {
+      nq_m = 0;
+      return;
+    }
     const int f = r;  // feature
     for (int e0 = 0; e0 < nq_m; e0 += 8) {
       int v[4];
@@ -262,7 +271,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
         v[u] = e < nq_m ? w_mq[e] : -1;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = (v[u] != -1 && f < F) ? w_rows[(v[u] & 0xFF) * F + f] : 0.f;
+      for (int u = 0; u < 4; ++u) x[u] = (v[u] != -1 && f < F) ? X[(r0 + (v[u] & 0xFF)) * F + f] : 0.f;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (v[u] == -1 || f >= F) continue;
@@ -285,6 +294,10 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   // nearest_centers bits: even features in .x, odd in .y, then .x + .y), and
   // the half's 32 lanes reduce to the top two (lowest index on ties)
   auto flush_r = [&](int64_t r0) {
+    if (MW_D2_VARIANT == 3) {
+      nq_r = 0;
+      return;
+    }
     for (int e0 = 0; e0 < nq_r; e0 += 2) {
       const int e = e0 + h;
       const bool ev = e < nq_r;
@@ -294,7 +307,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
       const int j = r;
       float dd = __builtin_inff();
       if (j < k) {
-        const float* xr = w_rows + row * F;
+        const float* xr = X + (r0 + row) * F;
         const float* cr = s_cenp[fi] + (size_t)j * F;
         f2v acc = f2v{0.f, 0.f};
         const int np = (F + 1) >> 1;  // pairs past F add exact zeros
@@ -324,7 +337,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
         lab = take ? plab : lab;
       }
       const bool on = ev && j == 0;
-      if (nq_m > 96) flush_m();
+      if (nq_m > 96) flush_m(r0);
       const int old = on ? (int)w_lab[fi * 32 + row] : 0;
       const bool ch = on && lab != old;
       if (ch) s_labp[fi][r0 + row] = (uint8_t)lab;
@@ -345,6 +358,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   // ---- chunk loads, one chunk ahead: lane (r, h) takes row r's features
   // 16 ks + 8 h + j (the B operand's); lane l < 2 nf the 16 labels of fit
   // l >> 1 at rows 16 (l & 1) .. + 15 (one buffer load: out of range reads 0)
+  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(X + lo * F, (hi > lo ? hi - lo : 0) * F * 4);  // this block's rows
   float xq[16];
   u4d lq = u4d{0u, 0u, 0u, 0u};
   const bool lq_on = lane < 2 * nf;
@@ -353,26 +367,14 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
     const int64_t r0 = lo + (int64_t)ci * 32;
     const int nrow = (int)min((int64_t)32, hi - r0);
     const int64_t rr = r0 + (r < nrow ? r : nrow - 1);
-    const float* xr = X + rr * F;
-    if ((F & 1) == 0) {
+    // buffer loads over the block's rows (out of range reads 0: no exec-mask
+    // branch per load, one address); features past F are zeroed in the B build
+    const int vo = (int)((rr - lo) * F) * 4;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const int f = 16 * ks + 8 * h + j;
-          const f2v v = f < F ? *reinterpret_cast<const f2v*>(xr + f) : f2v{0.f, 0.f};
-          xq[8 * ks + j] = v.x;
-          xq[8 * ks + j + 1] = v.y;
-        }
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int f = 16 * ks + 8 * h + j;
-          xq[8 * ks + j] = f < F ? xr[f] : 0.f;
-        }
-    }
+      for (int j = 0; j < 8; ++j)
+        xq[8 * ks + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, vo + (16 * ks + 8 * h + j) * 4, 0, 0));
     if (lq_on) {
       if (nrow == 32) {
         lq = *reinterpret_cast<const u4d*>(lq_base + r0 + (lane & 1) * 16);  // r0 % 32 == 0: aligned
@@ -390,7 +392,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
 
   int ci = wid;
   if (ci < nchunk) load_chunk(ci);
-  for (; ci < nchunk; ci += kD2Waves) {
+  for (; ci < nchunk; ci += nw) {
     const int64_t r0 = lo + (int64_t)ci * 32;
     const int nrow = (int)min((int64_t)32, hi - r0);
     const bool valid = r < nrow;
@@ -402,7 +404,6 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int f = 16 * ks + 8 * h + j;
-        if (f < F) w_rows[r * F + f] = xq[8 * ks + j];
         const float x = f < F ? __builtin_fmaf(xq[8 * ks + j], s_a[f], s_b[f]) : 0.f;
         bop[ks][j] = (_Float16)x;
         bol[ks][j] = (_Float16)(x - (float)bop[ks][j]);
@@ -422,8 +423,8 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
       bop[1][7] = h ? b31h : bop[1][7];
       bol[1][7] = h ? b31l : bol[1][7];
     }
-    if (ci + kD2Waves < nchunk) load_chunk(ci + kD2Waves);  // the next chunk's loads fly during this one
-    __builtin_amdgcn_wave_barrier();  // w_rows / w_lab written
+    if (ci + nw < nchunk) load_chunk(ci + nw);  // the next chunk's loads fly during this one
+    __builtin_amdgcn_wave_barrier();  // w_lab written
     // the old labels of the fits this lane decides (fi = h, h + 2, ...), packed
     // 4 per register (out of LDS once per chunk, not per close)
     constexpr int NLB = (kMaxFits + 1) / 2;
@@ -464,7 +465,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
         if (tie) w_rq[nq_r + __popcll(tm & ((1ull << lane) - 1ull))] = r | (fi << 8);
         nq_r = __builtin_amdgcn_readfirstlane(nq_r + (int)__popcll(tm));
       }
-      if (nq_m > 64) flush_m();
+      if (nq_m > 64) flush_m(r0);
       const int u = fA >> 1;
       const unsigned w = (u >> 2) == 0 ? olds[0] : ((u >> 2) == 1 ? olds[1] : olds[2]);
       const int old = (int)((w >> (8 * (u & 3))) & 0xFFu);
@@ -545,6 +546,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
           m1 = m2 = KMAX;
         }
         if (fi < 0) continue;
+        if (MW_D2_VARIANT == 2) continue;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v = acc[4 * j + i];  // (a bit_cast of the vector element itself reads element 0)
@@ -570,12 +572,17 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
         const int d1 = q == 0 ? pb1[0] : q == 1 ? pb1[1] : pb1[2];
         const int d2 = q == 0 ? pb2[0] : q == 1 ? pb2[1] : pb2[2];
         const int fq = __builtin_amdgcn_readfirstlane(q == 0 ? pf[0] : q == 1 ? pf[1] : pf[2]);
+#if MW_D2_VARIANT == 1
+        sink ^= c1 ^ c2 ^ d1 ^ d2 ^ fq;
+#else
         close2(c1, c2, d1, d2, fq);
+#endif
       }
     }
     flush_r(r0);
-    flush_m();
+    flush_m(r0);
   }
+  if (MW_D2_VARIANT == 1 && sink == 0x5a5a5a5a) s_chg[0] = 1;
   __syncthreads();
   // ---- records: per fit [dQ_hi kF | dQ_lo kF | dcount k | changed | recomputed | 0 | 0] ----
   for (int fi = 0; fi < nf; ++fi) {

@@ -532,6 +532,8 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
 
     # lloyd_dense2.h: F <= 30 (kD2MaxK 32); lloyd_dense.h: F <= 64, kDenseMaxFitK = 20
     dense_ok = USE_DENSE and F <= (64 if DENSE_MODE == "1" else 30) and max(ks) <= 20
+    if USE_C_FITS and not comm.sharded() and TRACE is None and not verbose:
+        return _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first, st)
     for it in range(max_iter):
         active = [g for g in range(n) if not fits[g].done]
         if not active:
@@ -590,6 +592,58 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
 
 
 LAST_STATS = {}  # diagnostics of the last lloyd_fits call (rows recomputed per fit)
+# lloyd_fits through the C++ driver (mw_lloyd_fits, csrc/fit.cpp) on one
+# process; MW_LLOYD_FITS_C=0 keeps the Python loop (A/B, per-launch trace)
+USE_C_FITS = os.environ.get("MW_LLOYD_FITS_C", "1") != "0"
+_PASS_NAMES = ["lloyd_pass_mode0_first", "lloyd_pass_mode0_tile", "lloyd_pass_mode0_queue",
+               "lloyd_pass_mode0_first_atomic", "lloyd_pass_mode0_list", "lloyd_pass_mode0_dense",
+               "lloyd_pass_mode0_dense", "lloyd_pass_mode1", "lloyd_pass_mode2"]
+
+
+def _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first, st):
+    """lloyd_fits' iterations in mw_lloyd_fits (the same host arithmetic and
+    pass-kind policy in C++: no Python between the passes)."""
+    S, F = rows.S, rows.F
+    n = len(fits)
+    ptrs = lambda ts: (C.c_void_p * n)(*[D.P(t) for t in ts])  # noqa: E731
+    h_k = np.array([fs.k for fs in fits], dtype=np.int32)
+    h_init = np.ascontiguousarray(np.concatenate([fs.centers.ravel() for fs in fits]), dtype=np.float64)
+    centers = np.empty_like(h_init)
+    inertia = np.empty(n, dtype=np.float64)
+    n_iter = np.empty(n, dtype=np.int32)
+    hist = np.zeros((n, max_iter, 2), dtype=np.int64)
+    hist_len = np.zeros(n, dtype=np.int32)
+    timing = np.zeros(27, dtype=np.float64) if profiling.enabled() else None
+    a32 = np.ascontiguousarray(rows.a_host, dtype=np.float32)
+    b32 = np.ascontiguousarray(rows.b_host, dtype=np.float32)
+    qexp = np.ascontiguousarray(rows.qexp, dtype=np.int32)
+    xmax = np.ascontiguousarray(rows.xmax, dtype=np.float32)
+    mu = np.ascontiguousarray(rows.mu, dtype=np.float64)
+    inv = np.ascontiguousarray(rows.inv, dtype=np.float64)
+    nobound = int(os.environ.get("MW_LLOYD_NOBOUND") == "1")
+    N.call("mw_lloyd_fits", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(rows.qexp_dev),
+           a32.ctypes.data, b32.ctypes.data, qexp.ctypes.data, xmax.ctypes.data, mu.ctypes.data,
+           inv.ctypes.data, n, h_k.ctypes.data, h_init.ctypes.data,
+           ptrs([fs.labels for fs in fits]), ptrs([fs.ub for fs in fits]), ptrs([fs.lb for fs in fits]),
+           ptrs([fs.ws for fs in fits]), D.P(par), D.P(out_all), int(max_iter), float(tol), int(first),
+           int(QUEUE_KIND), float(QUEUE_BELOW), int(DENSE_MIN_FITS) if dense_ok else 0, nobound,
+           centers.ctypes.data, inertia.ctypes.data, n_iter.ctypes.data, hist.ctypes.data, int(max_iter),
+           hist_len.ctypes.data, None if timing is None else timing.ctypes.data, st)
+    if timing is not None:
+        for slot, name in enumerate(_PASS_NAMES):
+            profiling.add_measured(name, int(timing[3 * slot]), timing[3 * slot + 1], timing[3 * slot + 2])
+    res = []
+    o = 0
+    for g, fs in enumerate(fits):
+        kF = fs.k * F
+        fs.centers = centers[o:o + kF].reshape(fs.k, F).copy()
+        o += kF
+        fs.history = [tuple(int(v) for v in h) for h in hist[g, :hist_len[g]]]
+        fs.recomputed = int(hist[g, :hist_len[g], 1].sum())
+        res.append((fs.labels, float(inertia[g]), fs.centers, int(n_iter[g])))
+    LAST_STATS["recomputed"] = [fs.recomputed for fs in fits]
+    LAST_STATS["history"] = [fs.history for fs in fits]
+    return res
 
 
 def lloyd_device(rows: DeviceRows, centers_init: np.ndarray, max_iter=300, tol=0.0, verbose=False,

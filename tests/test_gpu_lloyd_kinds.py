@@ -81,6 +81,38 @@ def test_pass_kinds_equal_full_estep(gpu, monkeypatch, C, size):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("dense", [True, False])
+def test_fits_driver_equals_python_loop(gpu, monkeypatch, dense):
+    """mw_lloyd_fits (the batched iterations in C++) against lloyd_fits'
+    Python loop: labels, centers, inertia, n_iter and every pass's (changed,
+    recomputed) bit for bit, with the dense pass and with the bounded kinds
+    only; an empty cluster is forced (duplicated initial centers) so the
+    relocation runs in both."""
+    from milwrm_amd import kmeans as KM
+
+    rows = _rows(30, 768)
+    rng = np.random.default_rng(3)
+    inits = []
+    for k in (2, 5, 9, 14, 20):
+        c = rows.scaled_rows(rng.choice(rows.S, size=k, replace=False))
+        if k >= 5:
+            c[1] = c[0]  # two identical centers: one of them ends empty
+        inits.append(c)
+    monkeypatch.setattr(KM, "USE_DENSE", dense)
+    out = {}
+    for name, use_c in [("py", False), ("c", True)]:
+        monkeypatch.setattr(KM, "USE_C_FITS", use_c)
+        res = KM.lloyd_fits(rows, [c.copy() for c in inits], 300, 1e-6)
+        out[name] = ([(r[0].cpu().numpy().copy(), r[1], r[2].copy(), r[3]) for r in res],
+                     [list(h) for h in KM.LAST_STATS["history"]])
+    for i, (a, b) in enumerate(zip(out["py"][0], out["c"][0])):
+        np.testing.assert_array_equal(b[0], a[0], err_msg=f"fit {i} labels")
+        np.testing.assert_array_equal(b[2], a[2], err_msg=f"fit {i} centers")
+        assert b[1] == a[1] and b[3] == a[3], f"fit {i}: inertia / n_iter {b[1], b[3]} vs {a[1], a[3]}"
+    assert out["c"][1] == out["py"][1]
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("outlier", [300.0, 3000.0])
 def test_dense_keys_far_rows_equal_full_estep(gpu, monkeypatch, outlier):
     """The dense pass's folded norms and keyed top two (lloyd_dense2.h) at
