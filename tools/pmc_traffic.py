@@ -52,7 +52,15 @@ KERNELS = {
 # reads FETCH_SIZE x 2 = 2.13 GB for 2.18 GB of algorithmic reads, so the x2
 # correction holds for it; over config 2's random draws x2 gives 6.17 GB =
 # two 128-B lines per straddling 120-B row plus one per random rank lookup.
-UNCALIBRATED = {"blur_sample", "sample_map", "lloyd_list", "lloyd_list_f64", "col_stats"}
+# Round 5 (tools/pmc_calib_r5.py, profiles/r05/calib/): over known draw patterns
+# blur_sample's FETCH_SIZE x 2 is 1.35x its algorithmic reads for sequential
+# and random draws alike (the blur's halo over-fetch, as the plain blur) and
+# its WRITE_SIZE is exact for sequential rows (1.19x for random 120-B rows);
+# sample_map's FETCH_SIZE x 2 is exact for sequential draws (random draws: a
+# 128-B line per rank lookup); col_stats_rows' FETCH_SIZE is exact WITHOUT
+# the x2 (its loads are not the wide streaming kind the correction is for).
+UNCALIBRATED = {"lloyd_list", "lloyd_list_f64"}
+FETCH_FACTOR = {"col_stats": 1}  # default 2
 
 
 def per_launch(path, pat):
@@ -70,15 +78,15 @@ def main():
     base = f"gpurun_out/pmc_{tag}"
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
                      f"'bench.py --steps 1 --warmup 1' ({base})",
-           "correction": "KB -> bytes; FETCH_SIZE x2 (gfx950 wide-read undercount); "
-                         "WRITE_SIZE as reported",
+           "correction": "KB -> bytes; FETCH_SIZE x2 (gfx950 wide-read undercount; x1 for "
+                         "col_stats_rows, calibrated round 5); WRITE_SIZE as reported",
            "kernels": {}}
     for name, pat in KERNELS.items():
         f, nf = per_launch(f"{base}/fetch/run_counter_collection.csv", pat)
         w, nw = per_launch(f"{base}/write/run_counter_collection.csv", pat)
         if f is None or w is None:
             continue
-        fb, wb = 2 * f * 1024, w * 1024
+        fb, wb = FETCH_FACTOR.get(name, 2) * f * 1024, w * 1024
         res["kernels"][name] = {"symbol": pat, "launches": nf, "fetch_bytes": fb, "write_bytes": wb,
                                 "traffic_bytes": fb + wb, "calibrated": name not in UNCALIBRATED}
     json.dump(res, open(out, "w"), indent=1)
