@@ -116,6 +116,15 @@ int mw_gather_rows(const float* d_img, int C, const int32_t* d_feat, int F,
 int mw_gather_rows_ri(const float* d_img, int C, const int32_t* d_feat, int F, const int32_t* d_idx,
                       const void* d_index, int64_t n_pix, int64_t pix_off, int64_t S, float* d_X, void* d_ws,
                       void* stream);
+/* The draws as pixels: d_idx[j] = pixel of rank d_idx[j] (+ pix_off) through
+ * the rank index, in place -- a pass over the draws that keeps the random
+ * lookups in the on-die caches (it runs beside the blur); then
+ * mw_gather_rows_px reads X[j, f] = img[d_pix[j], feat[f]] with no lookup.
+ * Same rows and records as mw_gather_rows over the same draws. */
+int mw_rank_to_pixel_ri(int32_t* d_idx, int64_t S, const void* d_index, int64_t n_pix, int64_t pix_off,
+                        void* stream);
+int mw_gather_rows_px(const float* d_img, int C, const int32_t* d_feat, int F, const int32_t* d_pix, int64_t S,
+                      float* d_X, void* d_ws, void* stream);
 /* Column statistics of rows already in X (same per-block records as
  * mw_gather_rows, same order: identical numbers for identical rows); then
  * mw_col_stats_finalize. */

@@ -300,6 +300,35 @@ def _assign_img_(image: img, features, centers, scaler, qc):
     return out(res)
 
 
+_SIDE = {}
+# 1: with the rank index, the draws become pixels before the gather (A/B;
+# device.py RANK_TABLE_MAX_PIX: no faster at config 2)
+GATHER_BY_PIXEL = os.environ.get("MW_GATHER_PX", "0") == "1"
+DRAWS_BESIDE = os.environ.get("MW_DRAWS_BESIDE", "1") != "0"  # 0: in line after the blur (A/B)
+
+
+def _draws_beside(M: int, fract: float, dev, after: torch.cuda.Event, index=None):
+    """``subsample_indices_device(M, fract, 16)`` issued on a side stream the
+    current stream then waits for: the MT19937 segments (compute) overlap
+    the blur (HBM) queued before them.  Same draws, same global-state replay.
+    ``index`` (a D.RankIndex): the draws are turned into pixels there too
+    (mw_rank_to_pixel_ri, lookups in the on-die caches), so the gather reads
+    rows with no dependent lookup."""
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE.get(str(dev))
+    if side is None:
+        side = _SIDE[str(dev)] = torch.cuda.Stream(device=dev)
+    side.wait_event(after)  # the work queued before the blur (not the blur)
+    with torch.cuda.stream(side):
+        idx, tot = subsample_indices_device(M, fract, 16, dev)
+        if index is not None:
+            D.rank_to_pixel(idx, index)
+    main.wait_stream(side)
+    idx.record_stream(main)
+    tot.record_stream(main)
+    return idx, tot
+
+
 def _gather_deferred(image: img, feat, idx, r2p, X_out) -> bool:
     """Subsample rows written by the blur itself for an image whose blur is
     deferred (D.defer_blur); False when it is not, or the fused kernel does
@@ -557,6 +586,8 @@ class mxif_labeler(tissue_labeler):
         # the first image's log-normalise + blur is queued before the host
         # work below (mask-rank counts, allocations), which then overlaps it
         batches = list(self.image_df["batch_names"])
+        ev0 = torch.cuda.Event()  # the work queued before this pass (see _draws_beside)
+        ev0.record()
         if images:
             images[0].log_normalize(mean=means[batches[0]])
             images[0].blurring(filter_name=filter_name, sigma=sigma)
@@ -578,6 +609,17 @@ class mxif_labeler(tissue_labeler):
         # sharding of the images over ranks, so the scaler is bitwise the same
         img_stats = torch.zeros((len(images), 1 + 2 * F), dtype=torch.float64, device=dev)
         xmax = torch.zeros(F, dtype=torch.float32, device=dev)  # column max |x| (Lloyd fixed point)
+        # the first image's draws do not depend on its pixels: issued now on a
+        # side stream, the generator runs beside the blur instead of after it
+        # materialised images gather by pixel: the draws become pixels through
+        # the rank index first (mw_rank_to_pixel_ri), not per row in the gather
+        def by_pixel(im, r2p):
+            return isinstance(r2p, D.RankIndex) and im._pending_blur is None and GATHER_BY_PIXEL
+
+        pre = None
+        if images and counts[0] and DRAWS_BESIDE:
+            px0 = by_pixel(images[0], ranks[0][0])
+            pre = _draws_beside(ranks[0][1], fract, dev, ev0, ranks[0][0] if px0 else None) + (px0,)
         # phase 2: fused lognorm+blur, gather rows into X (image_df order)
         off = 0
         paths = []
@@ -593,15 +635,24 @@ class mxif_labeler(tissue_labeler):
             if S:
                 if r2p is None:
                     r2p, _ = im._mask_rank()
-                idx, tot = subsample_indices_device(M, fract, 16, dev)
+                if n_img == 0 and pre is not None:
+                    idx, tot, px = pre
+                    pre = None
+                else:
+                    idx, tot = subsample_indices_device(M, fract, 16, dev)
+                    px = by_pixel(im, r2p)
+                    if px:
+                        D.rank_to_pixel(idx, r2p)
                 totals.append((tot, S))
                 feat = D.h2d(np.asarray(im._features(features), dtype=np.int32), dev)
                 if _gather_deferred(im, feat, idx, r2p, X[off:off + S]):
                     D.col_stats_rows(X[off:off + S], img_stats[n_img], accumulate=False,
                                      absmax=xmax)
                 else:
-                    D.gather_rows(D.as_float32(im._materialize()), feat, idx, r2p, X[off:off + S],
-                                  img_stats[n_img], accumulate=False, absmax=xmax)
+                    D.gather_rows(D.as_float32(im._materialize()), feat, idx, None if px else r2p,
+                                  X[off:off + S], img_stats[n_img], accumulate=False, absmax=xmax)
+                # slide-order keys: pixels or ranks (both monotone in the pixel)
+                # past the previous images' pixel counts
                 draws.append((off, S, idx, rank_base))
                 del idx
             else:
@@ -611,7 +662,7 @@ class mxif_labeler(tissue_labeler):
             r2p = None
             ranks[n_img] = (None, M)
             off += S
-            rank_base += M
+            rank_base += int(im.shape[0]) * int(im.shape[1])
             if use_path:
                 paths.append(_save_preprocessed(im, self.image_df["Img"].iloc[n_img], path_save))
         self._batch_counts = counts  # merged_batch_labels is built on first access

@@ -102,6 +102,8 @@ _PROTOS = {
     "mw_rank_index_bytes": (c_sz, [c_i64]),
     "mw_mask_rank_index": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mw_gather_rows_ri": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "mw_rank_to_pixel_ri": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp]),
+    "mw_gather_rows_px": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "mw_sample_map_ri": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "mw_sample_overflow_ri": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mw_slot_gather": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -32,7 +32,8 @@
 #pragma once
 
 // timing variants (tools/probe/d2_variants.sh; wrong results): 1 = no closes,
-// 2 = no key updates, 3 = no queue flushes
+// 2 = no key updates, 3 = no queue flushes, 4 = chunk loads + B operands only
+// (no tiles), 5 = chunk loads only
 #ifndef MW_D2_VARIANT
 #define MW_D2_VARIANT 0
 #endif
@@ -521,6 +522,16 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
         push(m1, m2, cur - 1);
       }
     };
+    if (MW_D2_VARIANT >= 4) {
+      float sk = xx;
+      if (MW_D2_VARIANT == 4)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sk += (float)bop[ks][j] + (float)bol[ks][j];
+      sink ^= __builtin_bit_cast(int, sk);
+      continue;
+    }
     for (int tt = 0; tt < ntile; ++tt) {
       const char* ap = s_A + ((size_t)(4 * tt) * 64 + lane) * 16;
       const h8x a0h = *reinterpret_cast<const h8x*>(ap);
@@ -582,7 +593,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
     flush_r(r0);
     flush_m(r0);
   }
-  if (MW_D2_VARIANT == 1 && sink == 0x5a5a5a5a) s_chg[0] = 1;
+  if (MW_D2_VARIANT != 0 && sink == 0x5a5a5a5a) s_chg[0] = 1;
   __syncthreads();
   // ---- records: per fit [dQ_hi kF | dQ_lo kF | dcount k | changed | recomputed | 0 | 0] ----
   for (int fi = 0; fi < nf; ++fi) {

@@ -583,7 +583,8 @@ __device__ __forceinline__ void chan_merge(double& n_a, double& m_a, double& q_a
 // partition and in the same order, so both give identical records.
 // RI: the sample -> pixel lookups through the rank index (rank_pixel, + pix_off)
 // instead of the rank -> pixel table r2p
-template <bool GATHER, bool RI = false>
+// PX: idx already holds pixels (mw_rank_to_pixel_ri ran on the draws)
+template <bool GATHER, bool RI = false, bool PX = false>
 __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ img, int C,
                                                      const int32_t* __restrict__ feat, int F,
                                                      const int32_t* __restrict__ idx,
@@ -592,7 +593,8 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
                                                      double* __restrict__ rec, RankIndexPtrs ix = {},
                                                      int64_t pix_off = 0) {
   auto pix_of = [&](int32_t rho) -> uint32_t {
-    if constexpr (RI) return rank_pixel(ix, (uint32_t)rho) + (uint32_t)pix_off;
+    if constexpr (PX) return (uint32_t)rho;
+    else if constexpr (RI) return rank_pixel(ix, (uint32_t)rho) + (uint32_t)pix_off;
     else return r2p[rho];
   };
   extern __shared__ __attribute__((aligned(16))) float s_tile[];  // 256*F floats + stats scratch
@@ -1088,6 +1090,52 @@ int mw_gather_rows_ri(const float* d_img, int C, const int32_t* d_feat, int F, c
   if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
   hipLaunchKernelGGL((gather_kernel<true, true>), dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_idx,
                      nullptr, S, R, d_X, reinterpret_cast<double*>(d_ws), rank_ptrs(d_index, n_pix), pix_off);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+// draws -> pixels in place through the rank index (several independent
+// lookups per lane in flight: the index sits in the on-die caches, so the
+// pass is latency-bound, not HBM-bound)
+__global__ void __launch_bounds__(256) rank_to_pixel_kernel(int32_t* __restrict__ idx, int64_t S,
+                                                            RankIndexPtrs ix, int64_t pix_off) {
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t j0 = (int64_t)blockIdx.x * 256 + threadIdx.x; j0 < S; j0 += U * stride) {
+    int32_t r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = j0 + u * stride < S ? idx[j0 + u * stride] : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (j0 + u * stride < S) idx[j0 + u * stride] = (int32_t)(rank_pixel(ix, (uint32_t)r[u]) + (uint32_t)pix_off);
+  }
+}
+
+int mw_rank_to_pixel_ri(int32_t* d_idx, int64_t S, const void* d_index, int64_t n_pix, int64_t pix_off,
+                        void* stream) {
+  MW_CHECK_ARG(d_idx && d_index, "mw_rank_to_pixel_ri: null pointer");
+  MW_CHECK_ARG(S >= 0 && n_pix > 0 && pix_off >= 0 && n_pix + pix_off <= 0x7fffffffll,
+               "mw_rank_to_pixel_ri: bad sizes S=%lld n_pix=%lld", (long long)S, (long long)n_pix);
+  if (S == 0) return MW_OK;
+  const int grid = (int)std::min<int64_t>((S + 1023) / 1024, 8192);
+  hipLaunchKernelGGL(rank_to_pixel_kernel, dim3(grid), dim3(256), 0, as_stream(stream), d_idx, S,
+                     rank_ptrs(d_index, n_pix), pix_off);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
+int mw_gather_rows_px(const float* d_img, int C, const int32_t* d_feat, int F, const int32_t* d_pix, int64_t S,
+                      float* d_X, void* d_ws, void* stream) {
+  MW_CHECK_ARG(d_img && d_feat && d_pix && d_X && d_ws, "mw_gather_rows_px: null pointer");
+  MW_CHECK_ARG(S > 0 && F > 0 && F <= 64 && C > 0, "mw_gather_rows_px: bad shape S=%lld F=%d",
+               (long long)S, F);
+  hipStream_t st = as_stream(stream);
+  const int G = stream_blocks(S);
+  const int64_t R = rows_per_block(S);
+  size_t lds = (size_t)kTile * F * sizeof(float);
+  if (lds < 4 * 256 * sizeof(double)) lds = 4 * 256 * sizeof(double);
+  hipLaunchKernelGGL((gather_kernel<true, false, true>), dim3(G), dim3(256), lds, st, d_img, C, d_feat, F, d_pix,
+                     nullptr, S, R, d_X, reinterpret_cast<double*>(d_ws), RankIndexPtrs{}, (int64_t)0);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

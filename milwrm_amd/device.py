@@ -307,7 +307,10 @@ class RankIndex:
 # per draw, the faster gather -- config 2: 1.67 vs 1.81 ms) for slides up to
 # RANK_TABLE_MAX_PIX pixels (1 GiB of table); the compact index above (config
 # 5's 40k x 40k slide: 0.27 GB instead of 6.4 GB).  MW_RANK_TABLE=1 / 0 forces
-# the table / the index.
+# the table / the index.  (Round 5, MW_GATHER_PX=1 with the index: the draws
+# turned into pixels beside the blur, then a lookup-free gather: gather 1.59
+# -> 1.22 ms, but the 17M index lookups take 1.2 ms on the side stream and
+# slow the blur by 0.65 ms: the step is unchanged, 17.65 vs 17.68 ms.)
 _RT = os.environ.get("MW_RANK_TABLE")
 RANK_TABLE_MAX_PIX = (1 << 62) if _RT == "1" else 0 if _RT == "0" else (1 << 28)
 
@@ -352,16 +355,19 @@ def mask_rank(mask_u8: torch.Tensor, pending=None):
 
 def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2p: torch.Tensor,
                 X_out: torch.Tensor, stats: torch.Tensor, accumulate: bool, absmax=None):
-    """X_out[j] = img[r2p[idx[j]], feat]; Chan-merge column stats into
-    ``stats`` = [n, mean[F], M2[F]] (fp64); max |x| per column maxed into
-    ``absmax`` (fp32 [F], optional)."""
+    """X_out[j] = img[r2p[idx[j]], feat] (``r2p`` None: idx holds the pixels,
+    rank_to_pixel); Chan-merge column stats into ``stats`` = [n, mean[F],
+    M2[F]] (fp64); max |x| per column maxed into ``absmax`` (fp32 [F],
+    optional)."""
     H, W, C = img_f32.shape
     S, F = X_out.shape
     if S == 0:
         return
     ws = WS.get("gather", N.query("mw_gather_ws_bytes", S, F))
     with profiling.timed("gather", S * (F * 4 * 2 + 8)):
-        if isinstance(r2p, RankIndex):
+        if r2p is None:
+            N.call("mw_gather_rows_px", P(img_f32), C, P(feat), F, P(idx), S, P(X_out), P(ws), stream())
+        elif isinstance(r2p, RankIndex):
             N.call("mw_gather_rows_ri", P(img_f32), C, P(feat), F, P(idx), P(r2p.buf), r2p.n_pix, r2p.pix_off,
                    S, P(X_out), P(ws), stream())
         else:
@@ -370,6 +376,15 @@ def gather_rows(img_f32: torch.Tensor, feat: torch.Tensor, idx: torch.Tensor, r2
     N.call("mw_col_stats_finalize", P(ws), S, F, P(stats), 1 if accumulate else 0, stream())
     if absmax is not None:
         N.call("mw_col_stats_absmax", P(ws), S, F, P(absmax), 1, stream())
+
+
+def rank_to_pixel(idx: torch.Tensor, index: "RankIndex"):
+    """idx[j] (tissue ranks, int32) -> their pixels (+ index.pix_off), in place."""
+    S = idx.numel()
+    if S:
+        with profiling.timed("rank_to_pixel", S * 8):
+            N.call("mw_rank_to_pixel_ri", P(idx), S, P(index.buf), index.n_pix, index.pix_off, stream())
+    return idx
 
 
 def col_stats_rows(X: torch.Tensor, stats: torch.Tensor, accumulate: bool, absmax=None):
