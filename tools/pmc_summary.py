@@ -26,7 +26,7 @@ SQ_KERNELS = {
     "kpp_pass": "kpp_pass_kernel<",
     "lloyd_pass": "lloyd_pass_kernel<",
     "lloyd_mark": "lloyd_mark_kernel",
-    "gather": "gather_kernel<true, false>",
+    "gather": "gather_kernel<true, false, false>",
     "col_stats_rows": "col_stats_rows_kernel",
     "nz_stats": "nz_stats_u16_kernel",
     "sample_map": "sample_map_kernel",
@@ -51,7 +51,8 @@ def main():
     base = f"gpurun_out/pmc_{tag}"
     res = {"source": f"rocprofv3 --pmc, separate passes (sq, mfma, fetch, write) over "
                      f"'bench.py --steps 1 --warmup 1' ({base})",
-           "correction": "KB -> bytes; FETCH_SIZE x2 (gfx950 wide-read undercount); WRITE_SIZE as reported",
+           "correction": "KB -> bytes; FETCH_SIZE x2 (gfx950 wide-read undercount; x1 for col_stats_rows, "
+                         "calibrated round 5); WRITE_SIZE as reported",
            "workload": workload, "kernels": {}, "sq": {},
            "sq_note": "SQ_* fractions of SQ_WAVE_CYCLES; mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / "
                       "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); separate rocprofv3 --pmc passes "
@@ -61,9 +62,10 @@ def main():
         w, nw = PT.per_launch(f"{base}/write/run_counter_collection.csv", pat)
         if f is None or w is None:
             continue
-        fb, wb = 2 * f * 1024, w * 1024
+        fb, wb = PT.FETCH_FACTOR.get(name, 2) * f * 1024, w * 1024
+        cal = name not in PT.UNCALIBRATED and not (name in PT.CALIBRATED_C2_ONLY and "c5" in tag)
         res["kernels"][name] = {"symbol": pat, "launches": nf, "fetch_bytes": fb, "write_bytes": wb,
-                                "traffic_bytes": fb + wb, "calibrated": name not in PT.UNCALIBRATED}
+                                "traffic_bytes": fb + wb, "calibrated": cal}
     sq = counters(base, "sq")
     mf = counters(base, "mfma")
     for name in SQ_KERNELS:
