@@ -228,9 +228,10 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   for (int q = t; q < ksum; q += blockDim.x) s_cnt[q] = 0;
   if (t < kMaxFits) s_chg[t] = s_rec[t] = 0;
   __syncthreads();
-  if (t < nf) {  // per fit: max |c|^2 (the decision bound)
+  if (t <= kMaxFits) {  // per fit: max |c|^2 (the decision bound); 0 past the fits
     float m = 0.f;
-    for (int s = s_off8[t]; s < s_off8[t] + s_k[t]; ++s) m = fmaxf(m, s_cc[s]);
+    if (t < nf)
+      for (int s = s_off8[t]; s < s_off8[t] + s_k[t]; ++s) m = fmaxf(m, s_cc[s]);
     s_cmax[t] = m;
   }
   __syncthreads();
@@ -240,13 +241,8 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   for (int i = 0; i < nf; ++i) cmax_all = fmaxf(cmax_all, s_cmax[i]);
   const bool big = !(cmax_all <= kD2NormMax);
 
-  // lane-indexed per-group / per-fit tables (read with v_readlane)
+  // lane-indexed fit of each 8-slot group (read with v_readlane: wave-uniform)
   const int v_fit8 = lane < kD2Groups ? s_fit8[lane] : -1;
-  const int v_k = lane < nf ? s_k[lane] : 0;
-  const int v_off8 = lane < nf ? s_off8[lane] : 0;
-  const int v_cmax = __builtin_bit_cast(int, lane < nf ? s_cmax[lane] : 0.f);
-  const uint64_t lpv = lane < nf ? (uint64_t)s_labp[lane] : 0ull;
-  const int v_lp_lo = (int)(unsigned)lpv, v_lp_hi = (int)(unsigned)(lpv >> 32);
   const int64_t lo = (int64_t)blk * da.R, hi = min(S, lo + da.R);
   const int nchunk = hi > lo ? (int)((hi - lo + 31) / 32) : 0;
   const int r = lane & 31, h = lane >> 5;
@@ -448,16 +444,15 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
       const int k2 = min(max(p, q), min((int)x2[0], (int)x2[1]));
       const int fB = fA + 1;
       const int fi = fA + h;
-      const int kA = __builtin_amdgcn_readlane(v_k, fA), kB = __builtin_amdgcn_readlane(v_k, fB);
-      const int oA = __builtin_amdgcn_readlane(v_off8, fA), oB = __builtin_amdgcn_readlane(v_off8, fB);
-      const int cA = __builtin_amdgcn_readlane(v_cmax, fA), cB = __builtin_amdgcn_readlane(v_cmax, fB);
-      const int kf = h ? kB : kA, o8 = h ? oB : oA;
+      // this lane's fit constants from LDS (two addresses per wave: broadcast reads)
+      const int kf = s_k[fi], o8 = s_off8[fi];
+      const float cmx = s_cmax[fi];
       const int t0 = o8 >> 5;
       const int tile = (((k1 >> 5) ^ t0) & 1) ? t0 + 1 : t0;
       const int lab = 32 * tile + (k1 & 31) - o8;
       const float acc1 = __builtin_bit_cast(float, (unsigned)k1 & kD2KeyMask);
       const float acc2 = __builtin_bit_cast(float, (unsigned)k2 & kD2KeyMask);
-      const float eb = kD2BScale * (xx + __builtin_bit_cast(float, h ? cB : cA)) + kD2BAbs;
+      const float eb = kD2BScale * (xx + cmx) + kD2BAbs;
       const bool act = valid && fi < nf;
       const bool tie = act && (far || (kf > 1 && !(acc1 - acc2 > 0.5f * eb)));
       const unsigned long long tm = __ballot(tie);
@@ -472,10 +467,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
       const int old = (int)((w >> (8 * (u & 3))) & 0xFFu);
       const bool on = act && !tie;
       const bool ch = on && lab != old;
-      const unsigned lo_a = (unsigned)__builtin_amdgcn_readlane(v_lp_lo, fA), lo_b = (unsigned)__builtin_amdgcn_readlane(v_lp_lo, fB);
-      const unsigned hi_a = (unsigned)__builtin_amdgcn_readlane(v_lp_hi, fA), hi_b = (unsigned)__builtin_amdgcn_readlane(v_lp_hi, fB);
-      uint8_t* const lp = reinterpret_cast<uint8_t*>(((uint64_t)(h ? hi_b : hi_a) << 32) | (h ? lo_b : lo_a));
-      if (ch) lp[r0 + r] = (uint8_t)lab;
+      if (ch) s_labp[fi][r0 + r] = (uint8_t)lab;  // (the pointer only where a label changed)
       if (da.bounds) {  // (kind 6 only): d = -2 (acc + delta)
         if (on && ((da.bounds >> fi) & 1)) {
           const float d1 = -2.f * (acc1 + delta), d2 = -2.f * (acc2 + delta);
