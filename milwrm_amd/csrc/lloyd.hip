@@ -33,6 +33,26 @@
 #include "kmeans_common.h"
 
 namespace mw {
+// Row blocks of the Lloyd passes.  At F <= 32 the tile, first, final and list
+// passes hold three blocks per CU, so 1024 blocks ran in 1.33 rounds (a
+// second round on a third of the chip); 3 x 256 CUs run in one: config-2 fit
+// 7.36 -> 7.20 ms (MW_KBLOCKS A/B, profiles/r05/grid/).  The passes' sums are
+// exact integers, so labels, centers and inertia do not depend on the grid
+// (k-means++ keeps kblocks: its fp64 potentials are summed per block).
+constexpr int kLloydBlocksF32 = 3 * 256;
+static inline int lloyd_blocks(int64_t S, int F) {
+  const int g = kblocks(S);
+  return (F <= 32 && g > kLloydBlocksF32) ? kLloydBlocksF32 : g;
+}
+static inline int64_t lloyd_rows(int64_t S, int F) {
+  int64_t tiles = (S + kT - 1) / kT;
+  if (tiles < 1) tiles = 1;
+  const int g = lloyd_blocks(S, F);
+  return ((tiles + g - 1) / g) * kT;
+}
+}  // namespace mw
+
+namespace mw {
 
 constexpr int kMaxFits = 24;
 constexpr float kEps = 1e-4f;  // bound-test margin (relative)
@@ -883,13 +903,13 @@ extern "C" {
 int mw_lloyd_rec_len(int k, int F) { return lloyd_rec(k, F); }
 
 size_t mw_lloyd_ws_bytes(int64_t S, int k, int F) {
-  const int G = kblocks(S);  // records, then the kList lengths and lists
-  return lloyd_list_off(G, k, F) + lloyd_al256((size_t)G * 4) + (size_t)G * krows(S) * 4 + 256;
+  const int G = lloyd_blocks(S, F);  // records, then the kList lengths and lists
+  return lloyd_list_off(G, k, F) + lloyd_al256((size_t)G * 4) + (size_t)G * lloyd_rows(S, F) * 4 + 256;
 }
 
 size_t mw_lloyd_ws_bytes_kinds(int64_t S, int k, int F, int with_list) {
   if (with_list && S < ((int64_t)1 << 31)) return mw_lloyd_ws_bytes(S, k, F);
-  return lloyd_list_off(kblocks(S), k, F) + 256;  // records only: kind 4 is never passed
+  return lloyd_list_off(lloyd_blocks(S, F), k, F) + 256;  // records only: kind 4 is never passed
 }
 
 int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream) {
@@ -944,8 +964,8 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
     return MW_EUNSUPPORTED;
   }
   hipStream_t s = as_stream(stream);
-  const int G = kblocks(S);
-  const int64_t R = krows(S);
+  const int G = lloyd_blocks(S, F);
+  const int64_t R = lloyd_rows(S, F);
   if (kind == kDense || kind == kDense + 1) {
     // dense x . C^T pass over every fit of the launch (lloyd_dense.h); kind 6
     // also writes the fits' distance bounds

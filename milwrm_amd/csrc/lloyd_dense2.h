@@ -624,7 +624,7 @@ static inline bool dense2_plan(const mw_lloyd_fit* h, int n, int64_t S, int F, D
   if (da.off8[n] > kD2Slots) return false;
   for (int g = n + 1; g <= kMaxFits; ++g) da.off8[g] = da.off8[n], da.coff[g] = da.coff[n];
   da.ntile = (da.off8[n] + 31) / 32;
-  int G = kblocks(S);  // never more records than the fits' workspaces hold
+  int G = lloyd_blocks(S, F);  // never more records than the fits' workspaces hold
   if (G > kD2MaxBlocks) G = kD2MaxBlocks;
   int64_t R = (S + G - 1) / G;
   R = (R + 31) & ~(int64_t)31;
