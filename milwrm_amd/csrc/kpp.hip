@@ -330,6 +330,27 @@ __device__ __forceinline__ void scan_blocks(const double* __restrict__ bs, int G
   }
 }
 
+// the same scan of n <= 4 arrays (array i at bs + i * G) at once: each
+// array gets the additions scan_blocks gives it, in the same order, under
+// one barrier pair per step for all of them (the search kernel's selection
+// scanned its T arrays one after another: 20 barriers each)
+__device__ __forceinline__ void scan_blocks4(const double* __restrict__ bs, int n, int G, double (*s)[1024]) {
+  const int t = threadIdx.x;  // blockDim = 1024 >= G
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s[i][t] = (i < n && t < G) ? bs[(size_t)i * G + t] : 0.0;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    double v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (i < n && t >= o) ? s[i][t - o] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < n) s[i][t] += v[i];
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(1024) kpp_pots_kernel(const double* __restrict__ bsum_cur,
                                                         int n_cur, int G, double* __restrict__ pots) {
   __shared__ double s[1024];
@@ -354,19 +375,21 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(
     int c_done, double u0, double u1, double u2, double u3, double u4, double u5, double u6,
     double u7, int T, int64_t* __restrict__ cand, int64_t* __restrict__ chosen,
     int* __restrict__ best_out, int best_given, const double* __restrict__ rv_given) {
-  __shared__ double s[1024];
+  __shared__ double s4[4][1024];
   __shared__ double s_pot[8];
   __shared__ double s_row[8][64];
   __shared__ int s_best;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int g_last = -1;  // first array of the group whose scans s4 holds
   if (best_given >= 0) {
     if (t == 0) { s_best = best_given; *best_out = best_given; }
     __syncthreads();
   } else {
-    for (int i = 0; i < n_cur; ++i) {
-      scan_blocks(bsum_cur + (size_t)i * G, G, s);
-      if (t == 0) s_pot[i] = s[G - 1];
+    for (int g0 = 0; g0 < n_cur; g0 += 4) {
+      scan_blocks4(bsum_cur + (size_t)g0 * G, min(4, n_cur - g0), G, s4);
+      if (t < 4 && g0 + t < n_cur) s_pot[g0 + t] = s4[t][G - 1];
       __syncthreads();
+      g_last = g0;
     }
     if (t == 0) {
       int b = 0;
@@ -380,7 +403,14 @@ __global__ void __launch_bounds__(1024) kpp_search_kernel(
   }
   const int b = s_best;
   if (T == 0) return;  // final selection only
-  scan_blocks(bsum_cur + (size_t)b * G, G, s);
+  // the best array's scan: still in s4 when its group was the last scanned
+  const double* s;
+  if (g_last >= 0 && b >= g_last && b < g_last + 4) {
+    s = s4[b - g_last];
+  } else {
+    scan_blocks4(bsum_cur + (size_t)b * G, 1, G, s4);
+    s = s4[0];
+  }
   if (w >= T) return;  // one wave per target from here on (no more barriers)
   const double pot = s[G - 1];
   const double us[8] = {u0, u1, u2, u3, u4, u5, u6, u7};
