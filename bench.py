@@ -79,6 +79,8 @@ def parse():
                          "label pipeline (BASELINE config 4)")
     ap.add_argument("--cpu-size", type=int, default=2048, help="oracle CPU-baseline slide side")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-outputs", action="store_true",
+                    help="skip the reference-format host outputs after the timed steps (timeline traces)")
     return ap.parse_args()
 
 
@@ -160,6 +162,20 @@ def make_step(slides, C, k, comm, sweep=False):
     return sweep_step
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo) and its logical CPU count."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return f"{name} ({os.cpu_count()} logical CPUs on the host; the baseline uses `cores` of them)"
+
+
 def cpu_baseline(size, C, k, sweep=False):
     """Oracle (numpy/scipy restatement of the reference pipeline) on a bounded
     host sample; pixels/s on this box's cores.  ``sweep``: the oracle's
@@ -182,7 +198,7 @@ def cpu_baseline(size, C, k, sweep=False):
         best = O.choose_best_k(Xs)
         dt = time.perf_counter() - t
         return dict(value=size * size / dt, unit="pixels/s", cores=int(threads), kind="port",
-                    sample=f"oracle choose_best_k (k=2..20) over the {Xs.shape[0]} rows of one "
+                    cpu_model=cpu_model(), sample=f"oracle choose_best_k (k=2..20) over the {Xs.shape[0]} rows of one "
                            f"{size}x{size}x{C} synthetic slide (best_k {best[0]}), {dt:.1f} s, "
                            f"numpy/OpenBLAS threads={threads}")
     raw, mask = O.synth_slide(size, size, C, seed=20251015, mode="hard")
@@ -190,7 +206,7 @@ def cpu_baseline(size, C, k, sweep=False):
     r = O.mxif_pipeline([raw], [mask], ["b"], list(range(C)), k=k)
     dt = time.perf_counter() - t
     return dict(value=size * size / dt, unit="pixels/s", cores=int(threads), kind="port",
-                sample=f"oracle mxif_pipeline on one {size}x{size}x{C} synthetic slide, k={k} "
+                cpu_model=cpu_model(), sample=f"oracle mxif_pipeline on one {size}x{size}x{C} synthetic slide, k={k} "
                        f"(n_iter {r['kmeans']['n_iter_']}), {dt:.1f} s, numpy/OpenBLAS threads="
                        f"{threads}")
 
@@ -304,6 +320,67 @@ def design_point(H, W, C, k, comm, lab_hard, steps=3):
             "ms_per_step": el / steps * 1e3, "value": H * W * steps / el, "unit": "pixels/s",
             "lloyd_iters": int(lab.kmeans.n_iter_),
             "kmeans_fit_ms": round(fit.get("total_ms", 0.0) / steps, 4)}
+
+
+FP32_PEAK_TFLOPS = 157.3    # MI355X vector / f32-matrix peak (MI355X_MICROARCH.md)
+F16_MFMA_PEAK_TFLOPS = 2500.0  # dense f16/bf16 matrix-core peak (spec, no sparsity)
+
+
+def dense_pass_roofline(rows, ks=tuple(range(9, 21)), reps=6):
+    """The sweep's ALU-bound kernel (the batched k-sweep E-step
+    against the ALU roofline): one dense Lloyd pass (lloyd_dense2.h) of the
+    fits k = 9..20 together over the sweep's own rows, timed with HIP events
+    on its stream.  Useful work = the x . c products every (row, center) pair
+    needs, S * sum(k) * F * 2 flops, against the fp32 peak (what a direct
+    fp32 E-step would issue); issued work = the f16 hi/lo matrix-core products
+    (per 32 rows: ceil(sum of 8-aligned k / 32) tiles x 6 v_mfma_f32_32x32x16_f16
+    of 32768 flops), against the f16 MFMA peak."""
+    from milwrm_amd import _native as N
+    from milwrm_amd import device as D
+    from milwrm_amd import kmeans as KM
+
+    S, F = rows.S, rows.F
+    if F > 30:
+        return None
+    rows.fixed_point()
+    dev = rows.X.device
+    rng = np.random.default_rng(5)
+    fits = [KM._FitState(rows, rows.scaled_rows(np.sort(rng.choice(S, size=k, replace=False))), dev)
+            for k in ks]
+    rls = [N.query("mw_lloyd_rec_len", k, F) for k in ks]
+    roff = np.concatenate([[0], np.cumsum(rls)]).astype(np.int64)
+    out_all = torch.zeros(int(roff[-1]), dtype=torch.float64, device=dev)
+    outs = [out_all[roff[g]:roff[g + 1]] for g in range(len(ks))]
+    poff = np.concatenate([[0], np.cumsum([k * F + 2 * k for k in ks])]).astype(np.int64)
+    host = np.zeros(int(poff[-1]), dtype=np.float32)
+    for g, fs in enumerate(fits):
+        host[int(poff[g]):int(poff[g]) + fs.k * F] = fs.centers.astype(np.float32).ravel()
+    par = D.h2d(host, dev)
+    st = D.stream()
+    sel = [(g, fits[g]) for g in range(len(ks))]
+    KM._launch_pass(rows, sel, 0, KM.KIND_FIRST, par, poff, outs, st)  # labels to start from
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ms = []
+    for it in range(reps + 1):
+        ev[0].record()
+        KM._launch_pass(rows, sel, 0, KM.KIND_DENSE, par, poff, outs, st)
+        ev[1].record()
+        torch.cuda.synchronize()
+        if it:
+            ms.append(ev[0].elapsed_time(ev[1]))
+    t = float(np.mean(ms)) * 1e-3
+    useful = float(S) * sum(ks) * F * 2
+    ntile = -(-sum((k + 7) // 8 * 8 for k in ks) // 32)
+    issued = float(-(-S // 32)) * ntile * 6 * 32768
+    nbytes = float(S) * F * 4 + 2.0 * S * len(ks)
+    del fits, out_all, outs
+    return {"kernel": "lloyd_dense2_kernel", "fits": list(ks), "rows": S, "ms": t * 1e3,
+            "useful_tflops": useful / t / 1e12, "fp32_peak_tflops": FP32_PEAK_TFLOPS,
+            "frac_fp32": useful / t / 1e12 / FP32_PEAK_TFLOPS,
+            "mfma_issued_tflops": issued / t / 1e12, "f16_mfma_peak_tflops": F16_MFMA_PEAK_TFLOPS,
+            "frac_f16_mfma": issued / t / 1e12 / F16_MFMA_PEAK_TFLOPS,
+            "hbm_GBps": nbytes / t / 1e9, "frac_hbm": nbytes / t / 1e9 / HBM_PEAK_GBPS}
 
 
 def host_outputs(lab):
@@ -478,6 +555,8 @@ def main():
                         "fit_passes": fit_passes, "lloyd_device_ms": pass_ms,
                         "device_ms_per_fit_pass": pass_ms / max(fit_passes, 1),
                         "curve": [float(v) for v in curve["Scaled Inertia"].values]}
+        if world == 1:
+            out["sweep"]["alu_roofline"] = dense_pass_roofline(lab._device_rows())
         out["config"]["workload"] = (f"find_optimal_k k=2..20 over {world} GPU(s) x {n_sl} synthetic "
                                      f"{C}-ch {H}x{W} slide(s) per GPU ({S_glob} rows; "
                                      f"{_config_name(H, W, C, n_sl, world, True)})")
@@ -492,7 +571,7 @@ def main():
         out["config"]["lloyd_iters"] = n_iter
         out["pipeline_roofline"] = {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,
                                     "unit": "GB/s", "frac": pipe_gbps / (HBM_PEAK_GBPS * world)}
-    if not args.sweep:
+    if not args.sweep and not args.no_host_outputs:
         out["host_outputs"] = host_outputs(lab)
     if (world == 1 and not args.sweep and args.mode == "hard" and not args.no_design_point
             and source == "device" and n_sl == 1 and H * W * C * 2 <= 20e9):

@@ -341,6 +341,21 @@ int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
                   int k, const double* h_init, uint32_t seed, int max_iter, double tol,
                   uint8_t* d_labels, double* h_centers, double* h_inertia, int* h_n_iter,
                   int64_t* h_init_idx, void* d_ws, size_t ws_bytes, void* stream);
+/* The same fit with an asynchronous end: returns once the final E-step
+ * (labels, inertia) is queued on `stream`, so the caller can queue the label
+ * pass behind it without a host round trip (the centers, n_iter and k-means++
+ * indices are final at return; d_labels is stream-ordered).  The final pass's
+ * record (mw_lloyd_rec_len(k, F) fp64) is copied to the caller's PAGE-LOCKED
+ * h_final_rec when the stream gets there; after synchronising the stream the
+ * inertia is (rec[rl - 2] * 2^32 + rec[rl - 1]) * 2^-(*h_inertia_exp).  A
+ * d_ws of NULL (workspace allocated inside) makes the end synchronous, with
+ * the same outputs. */
+int mw_kmeans_fit_async(const float* d_X, int64_t S, int F, const double* h_mu,
+                        const double* h_inv, const double* h_feature_var, const float* h_xmax,
+                        int k, const double* h_init, uint32_t seed, int max_iter, double tol,
+                        uint8_t* d_labels, double* h_centers, int* h_n_iter, int64_t* h_init_idx,
+                        void* d_ws, size_t ws_bytes, double* h_final_rec, int* h_inertia_exp,
+                        void* stream);
 
 /* ---- batched fits: the find_optimal_k sweep's Lloyd iterations ----------------
  * Replaces kMeansRes' per-k `KMeans(n_clusters=k, random_state=seed).fit(X)`
@@ -357,7 +372,7 @@ int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
  * d_ws[g] (mw_lloyd_ws_bytes); d_par: sum of (k F + 2k) fp32, d_out: sum of
  * mw_lloyd_rec_len(k, F) fp64.  Pass-kind policy: first_kind (0 or 3),
  * queue_kind (2 or 4) below queue_below of the rows recomputed, the dense pass
- * while >= dense_min fits run (0: never), nobound != 0: no bound ever holds.
+ * while >= dense_min fits run (< 0: never), nobound != 0: no bound ever holds.
  * Outputs: h_centers (the fits' k x F fp64 blocks), h_inertia[n],
  * h_n_iter[n]; h_hist (may be NULL): per fit hist_cap x (changed, recomputed)
  * int64, h_hist_len[n] entries; h_timing (may be NULL): 9 x (launches, ms,
@@ -374,6 +389,50 @@ int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_a32, const 
                   int64_t* h_hist, int hist_cap, int* h_hist_len, double* h_timing,
                   void* stream);
 
+/* ---- the same fits over row shards (one process per GPU) ----------
+ * Replaces the per-iteration loop of the row-sharded fit (MILWRM.py:706-737
+ * find_tissue_regions, MILWRM.py:29-90 the k sweep, with the pixels of a
+ * cohort split over the GPUs of a node): mw_lloyd_fits where each rank holds
+ * its S rows (ranks hold consecutive row ranges, `row_offset` its first global
+ * row, `rows_total` all of them) and the caller supplies the collectives.  Per
+ * pass ONE in-place sum over the ranks of the fits' records (exact
+ * fixed-point limbs, so the centers, labels, n_iter and inertia are bitwise
+ * those of one process over all rows); a rare empty-cluster relocation adds
+ * one all-gather of 2n values and one all-sum of n (F + 1) values.  Every
+ * rank calls with the same n, k, init, tolerances and policy, and S >= 1.
+ * The messages live in the caller's device buffer d_msg (fp64, msg_len >=
+ * mw_lloyd_fits_msg_len(sum of mw_lloyd_rec_len, F, world) elements), with
+ * d_out == d_msg (the records at offset 0); the callbacks address it by
+ * element offsets, return 0 on success, and must order the collective after
+ * the work queued on `stream` and the later work on `stream` after it (the
+ * Python package binds them to torch.distributed: RCCL on the current
+ * stream, or gloo through host copies; a C caller to ncclAllReduce /
+ * ncclAllGather on `stream`).  A failing callback ends the call with MW_EHIP. */
+typedef struct mw_fit_comm {
+  void* ctx;
+  int world;
+  int rank;
+  int64_t rows_total;
+  int64_t row_offset;
+  double* d_msg;
+  int64_t msg_len;
+  /* d_msg[off, off + n) <- its sum over the ranks */
+  int (*all_reduce_sum)(void* ctx, int64_t off, int64_t n, void* stream);
+  /* d_msg[out_off + r n, out_off + (r + 1) n) <- rank r's d_msg[in_off, in_off + n) */
+  int (*all_gather)(void* ctx, int64_t in_off, int64_t n, int64_t out_off, void* stream);
+} mw_fit_comm;
+int64_t mw_lloyd_fits_msg_len(int64_t rec_total, int F, int world);
+int mw_lloyd_fits_sharded(const float* d_X, int64_t S, int F, const float* d_a32, const float* d_b32,
+                          const int32_t* d_qexp, const float* h_a32, const float* h_b32,
+                          const int32_t* h_qexp, const float* h_xmax, const double* h_mu,
+                          const double* h_inv, int n, const int* h_k, const double* h_init,
+                          uint8_t* const* d_labels, float* const* d_ub, float* const* d_lb,
+                          void* const* d_ws, float* d_par, double* d_out, int max_iter, double tol,
+                          int first_kind, int queue_kind, double queue_below, int dense_min,
+                          int nobound, double* h_centers, double* h_inertia, int* h_n_iter,
+                          int64_t* h_hist, int hist_cap, int* h_hist_len, double* h_timing,
+                          const mw_fit_comm* comm, void* stream);
+
 /* ---- empty-cluster relocation support (_k_means_common.pyx:181-226) ---------
  * fp64 distance of every row to centers[labels]; returns the n largest
  * (value desc, index asc) into d_top_idx / d_top_val (n <= 64). */
@@ -386,8 +445,14 @@ int mw_farthest(const float* d_X, int64_t S, int F, const float* d_a,
 /* ---- label + confidence pass (MILWRM.py:237-277, 389-450) -------------------
  * Over n_pix HWC fp32 pixels (C channels, features d_feat[F]):
  * label = argmin_j ||x' - c_j||^2 (x' = x*a + b), conf = (d2 - d1)/d2;
- * mask == 0 → label -1, conf NaN.  Per-block [sum conf | count] per label go
- * to d_ws, mw_assign_reduce folds them into d_dom (fp64 [2k]). */
+ * mask == 0 → label -1, conf NaN.  Per-block records per label go to d_ws,
+ * mw_assign_reduce folds them into d_dom (fp64 [3k]) = [conf hi k | conf lo k
+ * | count k]: the per-domain sum of the confidences in exact fixed point,
+ * sum of rint(conf * 2^32) = hi * 2^32 + lo (value = that * 2^-32; NaN limbs
+ * when a confidence of the domain is NaN), and the pixel counts.  Every entry
+ * is an integer-valued fp64 below 2^53, so records of several launches (row
+ * bands, ranks) add exactly: the domain sums do not depend on how the pixels
+ * were split (reference: MILWRM.py:447-449, np.mean per domain). */
 size_t mw_assign_ws_bytes(int64_t n_pix, int k);
 int mw_assign_conf(const float* d_img, int C, const int32_t* d_feat, int F,
                    const float* d_a, const float* d_b, const float* d_centers,

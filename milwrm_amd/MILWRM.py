@@ -23,9 +23,9 @@ import torch
 
 from . import _native as N
 from . import device as D
-from .assign import (assign_image, assign_rows, banded_assign_image, blur_assign_image, dm_total,
-                     domain_means, domain_sse_deferred, domain_sse_image, domain_sse_rows,
-                     LabelPassQC)
+from .assign import (DOM_REC, assign_image, assign_rows, banded_assign_image, blur_assign_image,
+                     dm_total, dom_carry_, dom_sums, domain_means, domain_sse_deferred, domain_sse_image,
+                     domain_sse_rows, LabelPassQC)
 from .kmeans import DeviceRows, KMeans, StandardScaler, fit_many
 from .MxIF import checktype, img
 from .ST import blur_features_st
@@ -825,7 +825,7 @@ class mxif_labeler(tissue_labeler):
         k = int(self.k)
         if getattr(self, "_dom_dev", None):
             doms = self._slide_doms()
-            counts = doms[:, k:2 * k].T  # domains x images
+            counts = dom_sums(doms, k)[1].T  # domains x images
         else:
             counts = np.array([[np.sum(np.asarray(t) == j) for t in self.tissue_IDs]
                                for j in range(k)], dtype=np.float64)
@@ -843,25 +843,51 @@ class mxif_labeler(tissue_labeler):
         self.tissue_ID_proportion = df_count
         return _stacked_bar(df_count.T, cmap, figsize, "images", save_to)
 
-    def _slide_doms(self) -> np.ndarray:
-        """images x [per-domain confidence sums | pixel counts] from the label
-        pass; a slide split into row bands (milwrm_amd.bands) sums its bands."""
+    def _slide_doms_dev(self) -> torch.Tensor:
+        """images x domain records (exact limbs of the per-domain confidence
+        sums | pixel counts, ``dom_sums``) from the label pass, on the device;
+        a slide split into row bands (milwrm_amd.bands) sums its bands'
+        records exactly (one all-reduce over the ranks)."""
         t = torch.stack(self._dom_dev)
         ims = getattr(self, "_images", None) or []
         if ims and getattr(ims[0], "_band", None) is not None and self._comm.sharded():
-            t = self._comm.all_reduce_(t.clone())
-        return D.d2h(t)
+            t = dom_carry_(self._comm.all_reduce_(t.clone()))
+        return t
+
+    def _slide_doms(self) -> np.ndarray:
+        return D.d2h(self._slide_doms_dev())
 
     def confidence_score_images(self):
         """MILWRM.py:1868-1900 from the fused pass: confidence_IDs and the
-        images x domains DataFrame of mean confidences."""
+        images x domains DataFrame of mean confidences.  The frame is built on
+        first access of ``confidence_score_df`` from the domain records queued
+        here (no host round trip until it is read: the next slide's work can
+        be queued behind this one's label pass)."""
         k = self.kmeans.cluster_centers_.shape[0]
-        # images x domains, the frame the reference concatenates row by row
-        # (index 0..n-1, columns 0..k-1), built in one constructor call
-        doms = self._slide_doms() if self._dom_dev else np.zeros((0, 2 * k))
-        rows = [list(domain_means(dom, k).values()) for dom in doms]
+        t = self._slide_doms_dev() if self._dom_dev else None  # (its collective, if any, now)
+
+        def frame():
+            # images x domains, the frame the reference concatenates row by row
+            # (index 0..n-1, columns 0..k-1), built in one constructor call
+            doms = D.d2h(t) if t is not None else np.zeros((0, DOM_REC * k))
+            rows = [list(domain_means(dom, k).values()) for dom in doms]
+            return pd.DataFrame(np.asarray(rows, dtype=np.float64).reshape(-1, k))
+
         self.confidence_IDs = _LazyHostList(list(self._conf_dev), _conf_to_host)
-        self.confidence_score_df = pd.DataFrame(np.asarray(rows, dtype=np.float64).reshape(-1, k))
+        self._conf_df_pending = frame
+
+    @property
+    def confidence_score_df(self):
+        """MILWRM.py:1868-1900's images x domains frame of mean confidences."""
+        pending = self.__dict__.pop("_conf_df_pending", None)
+        if pending is not None:
+            self._confidence_score_df = pending()
+        return self._confidence_score_df
+
+    @confidence_score_df.setter
+    def confidence_score_df(self, value):
+        self.__dict__.pop("_conf_df_pending", None)
+        self._confidence_score_df = value
 
 
 class st_labeler(tissue_labeler):

@@ -70,10 +70,17 @@ _PROTOS = {
     "mw_kmeans_fit_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "mw_kmeans_fit": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_u32, c_i32,
                               C.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "mw_kmeans_fit_async": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_u32, c_i32,
+                                    C.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp]),
     "mw_lloyd_fits": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                               c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, C.c_double,
                               c_i32, c_i32, C.c_double, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp,
                               c_vp, c_vp]),
+    "mw_lloyd_fits_msg_len": (c_i64, [c_i64, c_i32, c_i32]),
+    "mw_lloyd_fits_sharded": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, C.c_double,
+                                      c_i32, c_i32, C.c_double, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32,
+                                      c_vp, c_vp, c_vp, c_vp]),
     "mw_farthest_ws_bytes": (c_sz, [c_i64]),
     "mw_farthest": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mw_assign_ws_bytes": (c_sz, [c_i64, c_i32]),
@@ -119,6 +126,19 @@ class LloydFit(C.Structure):
     _fields_ = [("centers", c_vp), ("drift", c_vp), ("half_sep", c_vp), ("labels", c_vp),
                 ("ub", c_vp), ("lb", c_vp), ("ws", c_vp), ("out", c_vp), ("k", c_i32),
                 ("drift_max", c_f32), ("inertia_exp", c_i32)]
+
+
+# mw_fit_comm's collectives (include/milwrm_amd.h): all_reduce_sum(ctx, off, n,
+# stream), all_gather(ctx, in_off, n, out_off, stream)
+ALL_REDUCE_SUM_FN = C.CFUNCTYPE(c_i32, c_vp, c_i64, c_i64, c_vp)
+ALL_GATHER_FN = C.CFUNCTYPE(c_i32, c_vp, c_i64, c_i64, c_i64, c_vp)
+
+
+class FitComm(C.Structure):
+    """``mw_fit_comm`` (include/milwrm_amd.h)."""
+    _fields_ = [("ctx", c_vp), ("world", c_i32), ("rank", c_i32), ("rows_total", c_i64),
+                ("row_offset", c_i64), ("d_msg", c_vp), ("msg_len", c_i64),
+                ("all_reduce_sum", ALL_REDUCE_SUM_FN), ("all_gather", ALL_GATHER_FN)]
 
 
 class NativeError(RuntimeError):

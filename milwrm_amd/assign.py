@@ -17,8 +17,10 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
     """One streaming pass over an HWC fp32 image.
 
     Returns (labels int8 [H,W] with -1 outside the mask, conf fp32 [H,W] with
-    NaN outside the mask, dom fp64 [2k] = per-label sum of confidences then
-    per-label pixel counts, both over mask != 0)."""
+    NaN outside the mask, dom fp64 [3k] = the per-label sums of confidences
+    as exact fixed-point limbs, then per-label pixel counts, both over mask
+    != 0: ``dom_sums`` reads them; records of several bands or ranks add
+    exactly)."""
     H, W, C = img_f32.shape
     k, F = centers.shape
     dev = img_f32.device
@@ -31,7 +33,7 @@ def assign_image(img_f32: torch.Tensor, feat_idx, mu, inv, centers: np.ndarray,
     lab = torch.empty((H, W), dtype=torch.int8, device=dev) if out_lab is None else out_lab
     conf = torch.empty((H, W), dtype=torch.float32, device=dev) if out_conf is None else out_conf
     assert lab.is_contiguous() and conf.is_contiguous() and lab.numel() == n and conf.numel() == n
-    dom = torch.empty(2 * k, dtype=torch.float64, device=dev)
+    dom = torch.empty(DOM_REC * k, dtype=torch.float64, device=dev)
     ws = D.WS.get("assign", N.query("mw_assign_ws_bytes", n, k))
     st = D.stream()
     with profiling.timed("assign_conf", n * (C * 4 + 1 + 5)):
@@ -80,7 +82,7 @@ def blur_assign_image(raw, sigma: float, inv_mean, pseudoval: float, mu, inv,
     D.FUSED_USED["assign"] += 1
     if not src.zero_copy:
         D.FUSED_USED["assign_streamed"] += 1
-    dom = torch.empty(2 * k, dtype=torch.float64, device=dev)
+    dom = torch.empty(DOM_REC * k, dtype=torch.float64, device=dev)
     ws = D.WS.get("assign", N.query("mw_assign_ws_bytes", n, k))
     st = D.stream()
     with profiling.timed("domain_records", n * 5):
@@ -156,7 +158,7 @@ def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
     dev = D.device()
     lab = torch.empty((r1 - r0, W), dtype=torch.int8, device=dev)
     conf = torch.empty((r1 - r0, W), dtype=torch.float32, device=dev)
-    dom = torch.zeros(2 * k, dtype=torch.float64, device=dev)
+    dom = torch.zeros(DOM_REC * k, dtype=torch.float64, device=dev)  # exact limbs: any band split, same bits
     buf, band_rows = _band_buffer(H, W, C, r, band_rows)
     for y0, y1, a, rb in bands(src, band_rows, r, r0, r1):
         out = buf[:rb.shape[0]]
@@ -164,7 +166,7 @@ def banded_assign_image(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
         _, _, d = assign_image(out[y0 - a:y1 - a], feat_idx, mu, inv, centers,
                                D.padded_mask(mask_u8[y0:y1].contiguous()),
                                out_lab=lab[y0 - r0:y1 - r0], out_conf=conf[y0 - r0:y1 - r0])
-        dom += d
+        dom_add_(dom, d)
         if qc is not None:  # the band is still in the buffer: its QC sums now
             qc.band(out[y0 - a:y1 - a], lab[y0 - r0:y1 - r0])
     D.FUSED_USED["assign_banded"] += 1
@@ -228,6 +230,7 @@ class _DomainSSE:
         self.out = [torch.zeros(N.query("mw_domain_sse_out_len", kc, F), dtype=torch.float64,
                                 device=dev) for _, kc in self.chunks]
         self.n = 0
+        self.n_adds = 0
 
     def add(self, img_f32: torch.Tensor, labels_i8: torch.Tensor):
         """Add the pixels of an HWC fp32 range (or fp64 rows as an S x 1 x F
@@ -236,6 +239,10 @@ class _DomainSSE:
         n = H * W
         if n == 0:
             return
+        self.n_adds += 1
+        if self.n_adds >= 1 << 10:  # every add puts < 2^43 into a limb: exact below 2^53
+            raise MemoryError("QC sums over 1023 pixel ranges or more would leave the exact limbs: "
+                              "the bands are too low for the HBM this slide needs")
         st = D.stream()
         f64 = img_f32.dtype == torch.float64
         for (d0, kc), c_d, out in zip(self.chunks, self.c_d, self.out):
@@ -359,6 +366,12 @@ def domain_sse_deferred(raw, sigma: float, inv_mean, pseudoval: float, feat_idx,
     dev = D.device()
     lab = _labels_i8(tissue_id, H * W, k, dev)
     buf, band_rows = _band_buffer(H, W, C, r, band_rows)
+    # the buffer may have come back lower than asked (alloc_rows halves on an
+    # out-of-memory error) and stream.bands may lower the bands again: the
+    # limb budget is checked on the bands actually summed (acc.add below)
+    if -(-H // max(1, band_rows)) >= 1 << 10:
+        raise MemoryError(f"the QC sums of this {H}-row slide need bands of >= {-(-H // 1023)} rows "
+                          f"for exact limbs and HBM holds {band_rows}")
 
     def bands():
         for y0, y1, a, rb in read_bands(src, band_rows, r):
@@ -448,7 +461,8 @@ def dm_total(s: dict) -> np.float64:
 
 def assign_rows(X: np.ndarray, centers: np.ndarray, mu=None, inv=None):
     """Assign host rows (S x F, already in the centers' space unless an
-    affine is given).  Returns (labels int64, conf fp64, dom fp64[2k])."""
+    affine is given).  Returns (labels int64, conf fp64, dom fp64[3k]
+    domain records, ``dom_sums``)."""
     X = np.ascontiguousarray(X, dtype=np.float32)
     S, F = X.shape
     dev = D.device()
@@ -461,11 +475,44 @@ def assign_rows(X: np.ndarray, centers: np.ndarray, mu=None, inv=None):
             conf.reshape(-1).cpu().numpy().astype(np.float64), dom.cpu().numpy())
 
 
+DOM_REC = 3  # label-pass domain records: [conf hi k | conf lo k | count k] (mw_assign_reduce)
+_TWO32 = 4294967296.0
+
+
+def dom_add_(dom: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+    """dom += d for label-pass domain records (integer-valued fp64 limbs),
+    with the lo limbs' carries moved into the hi limbs so that any number of
+    bands stays exact (every entry below 2^53)."""
+    dom += d
+    return dom_carry_(dom)
+
+
+def dom_carry_(dom: torch.Tensor) -> torch.Tensor:
+    """Move the lo limbs' carries of domain records into their hi limbs (in
+    place, exact): after adding records of several bands or ranks."""
+    k = dom.shape[-1] // DOM_REC
+    carry = torch.floor(dom[..., k:2 * k] / _TWO32)
+    dom[..., :k] += carry
+    dom[..., k:2 * k] -= carry * _TWO32
+    return dom
+
+
+def dom_sums(dom, k: int):
+    """(per-domain sums of the confidences, pixel counts) as fp64 from the
+    records: one rounding of the exact fixed-point total, so the same bits
+    for any split of the pixels."""
+    d = np.asarray(dom, dtype=np.float64)
+    s = (d[..., :k] * _TWO32 + d[..., k:2 * k]) * 2.0 ** -32
+    return s, d[..., 2 * k:3 * k]
+
+
 def domain_means(dom: np.ndarray, k: int) -> dict:
-    """Per-domain mean confidence ``np.mean(cID[tissue_ID == i])``: NaN for an
-    empty domain (numpy's mean of an empty slice)."""
+    """Per-domain mean confidence ``np.mean(cID[tissue_ID == i])`` from the
+    label pass's records: NaN for an empty domain (numpy's mean of an empty
+    slice)."""
+    s, cnt = dom_sums(dom, k)
     out = {}
     for i in range(k):
-        n = dom[k + i]
-        out[i] = float(dom[i] / n) if n > 0 else float("nan")
+        n = cnt[i]
+        out[i] = float(s[i] / n) if n > 0 else float("nan")
     return out

@@ -16,6 +16,7 @@
 // (np_sum) so the host arithmetic matches it bit for bit.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -172,9 +173,17 @@ int dev_alloc(DevBuf& b, size_t n) {
 // that follows its previous copy.
 constexpr size_t kPinTab = 0, kPinRec = 32 << 10, kPinRows = 160 << 10, kPinSetup = 176 << 10,
                  kPinIdx = 178 << 10, kPinBytes = 180 << 10;
+// A fit that returns before its last copies ran (mw_kmeans_fit_async)
+// records this event after them: the next user of the staging waits for it.
+static thread_local hipEvent_t pin_busy = nullptr;
 static char* pinned_staging() {
   static thread_local char* p = nullptr;
   if (!p && hipHostMalloc(reinterpret_cast<void**>(&p), kPinBytes, 0) != hipSuccess) p = nullptr;
+  if (pin_busy) {
+    (void)hipEventSynchronize(pin_busy);
+    (void)hipEventDestroy(pin_busy);
+    pin_busy = nullptr;
+  }
   return p;
 }
 
@@ -281,6 +290,26 @@ struct Fit {
     return MW_OK;
   }
 
+  // pass() without the download's wait: the record goes to the caller's
+  // page-locked h_rec when the stream gets there
+  int pass_async(int mode, int kind, int iexp, double* h_rec) {
+    mw_lloyd_fit f{};
+    f.centers = par;
+    f.drift = par + (size_t)k * F;
+    f.half_sep = par + (size_t)k * F + k;
+    f.labels = labels;
+    f.ub = ub;
+    f.lb = lb;
+    f.ws = ws;
+    f.out = out;
+    f.k = k;
+    f.drift_max = drift_max;
+    f.inertia_exp = iexp;
+    MW_TRY(mw_lloyd_pass(X, S, F, a32, b32, qexp, 1, &f, mode, kind, st));
+    MW_HIP(hipMemcpyAsync(h_rec, out, rl * sizeof(double), hipMemcpyDeviceToHost, st));
+    return MW_OK;
+  }
+
   // the same for indices on the device (idx[0] = first when first >= 0): one
   // gather kernel into `tmp` (n x F floats of device scratch) and one copy
   int scaled_rows_dev(const int64_t* d_idx, int64_t first, int n, const double* mu, const double* inv,
@@ -362,11 +391,40 @@ extern "C" size_t mw_kmeans_fit_ws_bytes(int64_t S, int F, int k) {
   return fit_layout(S, F, k).total;
 }
 
+static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_mu, const double* h_inv,
+                           const double* h_feature_var, const float* h_xmax, int k, const double* h_init,
+                           uint32_t seed, int max_iter, double tol, uint8_t* d_labels, double* h_centers,
+                           double* h_inertia, int* h_n_iter, int64_t* h_init_idx, void* d_ws, size_t ws_bytes,
+                           double* h_final_rec, int* h_inertia_exp, void* stream);
+
 extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
                              const double* h_inv, const double* h_feature_var, const float* h_xmax,
                              int k, const double* h_init, uint32_t seed, int max_iter, double tol,
                              uint8_t* d_labels, double* h_centers, double* h_inertia, int* h_n_iter,
                              int64_t* h_init_idx, void* d_ws, size_t ws_bytes, void* stream) {
+  return kmeans_fit_impl(d_X, S, F, h_mu, h_inv, h_feature_var, h_xmax, k, h_init, seed, max_iter, tol,
+                         d_labels, h_centers, h_inertia, h_n_iter, h_init_idx, d_ws, ws_bytes, nullptr, nullptr,
+                         stream);
+}
+
+extern "C" int mw_kmeans_fit_async(const float* d_X, int64_t S, int F, const double* h_mu,
+                                   const double* h_inv, const double* h_feature_var, const float* h_xmax,
+                                   int k, const double* h_init, uint32_t seed, int max_iter, double tol,
+                                   uint8_t* d_labels, double* h_centers, int* h_n_iter, int64_t* h_init_idx,
+                                   void* d_ws, size_t ws_bytes, double* h_final_rec, int* h_inertia_exp,
+                                   void* stream) {
+  MW_CHECK_ARG(h_final_rec && h_inertia_exp, "mw_kmeans_fit_async: null final-record pointer");
+  double unused = 0.0;
+  return kmeans_fit_impl(d_X, S, F, h_mu, h_inv, h_feature_var, h_xmax, k, h_init, seed, max_iter, tol,
+                         d_labels, h_centers, &unused, h_n_iter, h_init_idx, d_ws, ws_bytes, h_final_rec,
+                         h_inertia_exp, stream);
+}
+
+static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_mu, const double* h_inv,
+                           const double* h_feature_var, const float* h_xmax, int k, const double* h_init,
+                           uint32_t seed, int max_iter, double tol, uint8_t* d_labels, double* h_centers,
+                           double* h_inertia, int* h_n_iter, int64_t* h_init_idx, void* d_ws, size_t ws_bytes,
+                           double* h_final_rec, int* h_inertia_exp, void* stream) {
   MW_CHECK_ARG(d_X && h_mu && h_inv && d_labels && h_centers && h_inertia && h_n_iter,
                "mw_kmeans_fit: null pointer");
   MW_CHECK_ARG(F >= 1 && F <= 64, "mw_kmeans_fit: F=%d outside [1, 64]", F);
@@ -636,11 +694,30 @@ extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h
   const double xc = xnorm + cmax;
   const int iexp = exp_below(xc * xc * 1.01);
   MW_TRY(fit.upload(centers));
+  *h_n_iter = n_iter;
+  std::memcpy(h_centers, centers.data(), centers.size() * sizeof(double));
+  if (h_final_rec && !own.p && pinned_staging()) {  // (a workspace allocated here is freed on return: synchronous end)
+    // asynchronous end: the final pass and its record's copy into the caller's
+    // page-locked h_final_rec are queued; the caller reads the inertia,
+    // (rec[rl - 2] * 2^32 + rec[rl - 1]) * 2^-iexp, after `stream` reaches
+    // here (the labels likewise: stream-ordered).  The staging the table came
+    // from stays busy until then.
+    MW_TRY(fit.pass_async(strict ? 2 : 1, 0, iexp, h_final_rec));
+    *h_inertia_exp = iexp;
+    hipEvent_t ev;
+    MW_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    MW_HIP(hipEventRecord(ev, st));
+    pin_busy = ev;
+    *h_inertia = std::numeric_limits<double>::quiet_NaN();
+    return MW_OK;
+  }
   MW_TRY(fit.pass(strict ? 2 : 1, 0, iexp, rec));
   const double* tail = rec.data() + fit.rl - 4;
   *h_inertia = (tail[2] * 4294967296.0 + tail[3]) * std::ldexp(1.0, -iexp);
-  *h_n_iter = n_iter;
-  std::memcpy(h_centers, centers.data(), centers.size() * sizeof(double));
+  if (h_final_rec) {
+    std::memcpy(h_final_rec, rec.data(), (size_t)fit.rl * sizeof(double));
+    *h_inertia_exp = iexp;
+  }
   return MW_OK;
 }
 
@@ -726,6 +803,47 @@ void fits_tables(FitsFit& fs, int F, bool nobound, float* h) {
   }
 }
 
+// Message layout of a sharded run in the caller's d_msg (fp64): the fits'
+// records (d_out == d_msg) | the local top-64 (distance, global row) pairs of
+// a relocation | their all-gather (world x 64 pairs) | the winners' (raw row,
+// old label) from their owners (64 x (F + 1)).
+struct MsgLayout {
+  int64_t vi, gathered, owners, total;
+};
+MsgLayout msg_layout(int64_t rec_total, int F, int world) {
+  MsgLayout L;
+  L.vi = rec_total;
+  L.gathered = L.vi + 2 * 64;
+  L.owners = L.gathered + (int64_t)world * 2 * 64;
+  L.total = L.owners + 64 * (int64_t)(F + 1);
+  return L;
+}
+
+// hipEvent pairs of the per-launch timing, destroyed on every return path
+struct TimedLaunches {
+  struct T {
+    hipEvent_t a, b;
+    int slot;
+    double bytes;
+  };
+  std::vector<T> v;
+  ~TimedLaunches() {
+    for (T& t : v) {
+      (void)hipEventDestroy(t.a);
+      (void)hipEventDestroy(t.b);
+    }
+  }
+};
+
+int lloyd_fits_impl(const float* d_X, int64_t S, int F, const float* d_a32, const float* d_b32,
+                    const int32_t* d_qexp, const float* h_a32, const float* h_b32, const int32_t* h_qexp,
+                    const float* h_xmax, const double* h_mu, const double* h_inv, int n, const int* h_k,
+                    const double* h_init, uint8_t* const* d_labels, float* const* d_ub, float* const* d_lb,
+                    void* const* d_ws, float* d_par, double* d_out, int max_iter, double tol, int first_kind,
+                    int queue_kind, double queue_below, int dense_min, int nobound, double* h_centers,
+                    double* h_inertia, int* h_n_iter, int64_t* h_hist, int hist_cap, int* h_hist_len,
+                    double* h_timing, const mw_fit_comm* comm, void* stream);
+
 }  // namespace
 }  // namespace mw
 
@@ -739,6 +857,51 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
                              int nobound, double* h_centers, double* h_inertia, int* h_n_iter,
                              int64_t* h_hist, int hist_cap, int* h_hist_len, double* h_timing,
                              void* stream) {
+  return lloyd_fits_impl(d_X, S, F, d_a32, d_b32, d_qexp, h_a32, h_b32, h_qexp, h_xmax, h_mu, h_inv, n, h_k,
+                         h_init, d_labels, d_ub, d_lb, d_ws, d_par, d_out, max_iter, tol, first_kind, queue_kind,
+                         queue_below, dense_min, nobound, h_centers, h_inertia, h_n_iter, h_hist, hist_cap,
+                         h_hist_len, h_timing, nullptr, stream);
+}
+
+extern "C" int64_t mw_lloyd_fits_msg_len(int64_t rec_total, int F, int world) {
+  if (rec_total < 0 || F < 1 || F > 64 || world < 1) return 0;
+  return msg_layout(rec_total, F, world).total;
+}
+
+extern "C" int mw_lloyd_fits_sharded(const float* d_X, int64_t S, int F, const float* d_a32,
+                                     const float* d_b32, const int32_t* d_qexp, const float* h_a32,
+                                     const float* h_b32, const int32_t* h_qexp, const float* h_xmax,
+                                     const double* h_mu, const double* h_inv, int n, const int* h_k,
+                                     const double* h_init, uint8_t* const* d_labels, float* const* d_ub,
+                                     float* const* d_lb, void* const* d_ws, float* d_par, double* d_out,
+                                     int max_iter, double tol, int first_kind, int queue_kind,
+                                     double queue_below, int dense_min, int nobound, double* h_centers,
+                                     double* h_inertia, int* h_n_iter, int64_t* h_hist, int hist_cap,
+                                     int* h_hist_len, double* h_timing, const mw_fit_comm* comm,
+                                     void* stream) {
+  MW_CHECK_ARG(comm && comm->d_msg && comm->all_reduce_sum && comm->all_gather,
+               "mw_lloyd_fits_sharded: null comm");
+  MW_CHECK_ARG(comm->world >= 1 && comm->rank >= 0 && comm->rank < comm->world && comm->row_offset >= 0 &&
+                   comm->rows_total >= S + comm->row_offset,
+               "mw_lloyd_fits_sharded: bad world / rank / row range");
+  MW_CHECK_ARG(d_out == comm->d_msg, "mw_lloyd_fits_sharded: d_out must be comm->d_msg (records at offset 0)");
+  return lloyd_fits_impl(d_X, S, F, d_a32, d_b32, d_qexp, h_a32, h_b32, h_qexp, h_xmax, h_mu, h_inv, n, h_k,
+                         h_init, d_labels, d_ub, d_lb, d_ws, d_par, d_out, max_iter, tol, first_kind, queue_kind,
+                         queue_below, dense_min, nobound, h_centers, h_inertia, h_n_iter, h_hist, hist_cap,
+                         h_hist_len, h_timing, comm, stream);
+}
+
+namespace mw {
+namespace {
+
+int lloyd_fits_impl(const float* d_X, int64_t S, int F, const float* d_a32, const float* d_b32,
+                    const int32_t* d_qexp, const float* h_a32, const float* h_b32, const int32_t* h_qexp,
+                    const float* h_xmax, const double* h_mu, const double* h_inv, int n, const int* h_k,
+                    const double* h_init, uint8_t* const* d_labels, float* const* d_ub, float* const* d_lb,
+                    void* const* d_ws, float* d_par, double* d_out, int max_iter, double tol, int first_kind,
+                    int queue_kind, double queue_below, int dense_min, int nobound, double* h_centers,
+                    double* h_inertia, int* h_n_iter, int64_t* h_hist, int hist_cap, int* h_hist_len,
+                    double* h_timing, const mw_fit_comm* comm, void* stream) {
   MW_CHECK_ARG(d_X && d_a32 && d_b32 && d_qexp && h_a32 && h_b32 && h_qexp && h_xmax && h_mu && h_inv &&
                    h_k && h_init && d_labels && d_ub && d_lb && d_ws && d_par && d_out && h_centers &&
                    h_inertia && h_n_iter,
@@ -746,6 +909,8 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
   MW_CHECK_ARG(n >= 1 && F >= 1 && F <= 64 && S >= 1 && max_iter >= 1 && tol >= 0.0,
                "mw_lloyd_fits: bad n / F / S / max_iter / tol");
   hipStream_t st = as_stream(stream);
+  // rows over all shards (the pass-kind policy compares the global recomputed count with it)
+  const int64_t S_glob = comm ? comm->rows_total : S;
   std::vector<FitsFit> fits(n);
   std::vector<int64_t> poff(n + 1, 0), roff(n + 1, 0);
   size_t coff = 0;
@@ -770,7 +935,7 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
   }
   int kmax = 1;
   for (int g = 0; g < n; ++g) kmax = std::max(kmax, h_k[g]);
-  const bool dense_ok = dense_min > 0 && kmax <= 20;  // (the caller checks F)
+  const bool dense_ok = dense_min >= 0 && kmax <= 20;  // dense_min < 0: never (the caller checks F)
 
   // host staging: pinned when the tables / records fit its regions
   char* pin = pinned_staging();
@@ -796,18 +961,7 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
   }
 
   // per-launch timing (bench.py's profiling): slot = kind (mode 0) or 6 + mode
-  struct Timed {
-    hipEvent_t a, b;
-    int slot;
-    double bytes;
-  };
-  std::vector<Timed> timed;
-  auto ev_fail = [&]() {
-    for (Timed& t : timed) {
-      (void)hipEventDestroy(t.a);
-      (void)hipEventDestroy(t.b);
-    }
-  };
+  TimedLaunches timed;
 
   auto upload = [&](const std::vector<int>& sel) -> int {
     for (int g : sel) fits_tables(fits[g], F, nobound != 0, host_par + poff[g]);
@@ -841,13 +995,17 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
         else
           nbytes += 9.0 * S + ((mode || (kind != 2 && kind != 4)) ? (double)S * F * 4 : 0.0);
       }
-      Timed t{};
+      TimedLaunches::T t{};
       if (h_timing) {
         MW_HIP(hipEventCreate(&t.a));
-        MW_HIP(hipEventCreate(&t.b));
+        if (hipEventCreate(&t.b) != hipSuccess) {
+          (void)hipEventDestroy(t.a);
+          set_error("mw_lloyd_fits: hipEventCreate failed");
+          return MW_EHIP;
+        }
         t.slot = mode ? 6 + mode : kind;
         t.bytes = nbytes;
-        timed.push_back(t);
+        timed.v.push_back(t);
         MW_HIP(hipEventRecord(t.a, st));
       }
       MW_TRY(mw_lloyd_pass(d_X, S, F, d_a32, d_b32, d_qexp, (int)arr.size(), arr.data(), mode, kind, st));
@@ -855,11 +1013,23 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
     }
     return MW_OK;
   };
+  // the caller's collectives (sharded rows): a failing callback ends the fit
+  auto comm_call = [&](int rc_cb, const char* what) -> int {
+    if (rc_cb == 0) return MW_OK;
+    set_error("mw_lloyd_fits_sharded: the %s callback returned %d", what, rc_cb);
+    return MW_EHIP;
+  };
+  // one all-reduce of the exact records over the shards (the only exchange of
+  // a pass), then one download
   auto download = [&]() -> int {
+    if (comm) MW_TRY(comm_call(comm->all_reduce_sum(comm->ctx, 0, roff[n], stream), "all_reduce_sum"));
     MW_HIP(hipMemcpyAsync(rec, d_out, rec_bytes, hipMemcpyDeviceToHost, st));
     MW_HIP(hipStreamSynchronize(st));
     return MW_OK;
   };
+  const MsgLayout ML = msg_layout(roff[n], F, comm ? comm->world : 1);
+  if (comm) MW_CHECK_ARG(comm->msg_len >= ML.total, "mw_lloyd_fits_sharded: msg_len %lld < %lld",
+                         (long long)comm->msg_len, (long long)ML.total);
 
   // relocation scratch (allocated on the first empty cluster)
   DevBuf far_buf;
@@ -890,7 +1060,7 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
       } else if (!fs.bounds_ok) {
         kind = kKindTile;
       } else {
-        double frac = (double)fs.hist.back() / (double)std::max<int64_t>(S, 1);
+        double frac = (double)fs.hist.back() / (double)std::max<int64_t>(S_glob, 1);
         if (fs.prev_dmax > 0 && std::isfinite(fs.drift_max)) frac *= std::min(1.0, fs.drift_max / fs.prev_dmax);
         kind = frac > queue_below ? kKindTile : queue_kind;
       }
@@ -941,25 +1111,90 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
           d_topv = reinterpret_cast<double*>(d_topi + 64);
         }
         MW_HIP(hipMemcpyAsync(d_c64, fs.centers.data(), fs.centers.size() * 8, hipMemcpyHostToDevice, st));
-        if ((rc = mw_farthest(d_X, S, F, d_a32, d_b32, d_c64, k, d_labels[g], ne, d_topi, d_topv, d_farws,
+        const int m = (int)std::min<int64_t>(ne, S);  // this shard's candidates (S >= 1)
+        if ((rc = mw_farthest(d_X, S, F, d_a32, d_b32, d_c64, k, d_labels[g], m, d_topi, d_topv, d_farws,
                               st)) != MW_OK)
           break;
-        std::vector<int64_t> far_i(ne);
-        std::vector<double> far_v(ne);
-        MW_HIP(hipMemcpyAsync(far_i.data(), d_topi, ne * 8, hipMemcpyDeviceToHost, st));
-        MW_HIP(hipMemcpyAsync(far_v.data(), d_topv, ne * 8, hipMemcpyDeviceToHost, st));
+        std::vector<int64_t> far_i(m);
+        std::vector<double> far_v(m);
+        MW_HIP(hipMemcpyAsync(far_i.data(), d_topi, m * 8, hipMemcpyDeviceToHost, st));
+        MW_HIP(hipMemcpyAsync(far_v.data(), d_topv, m * 8, hipMemcpyDeviceToHost, st));
         MW_HIP(hipStreamSynchronize(st));
-        double vmax = far_v[0];
-        for (double v : far_v) vmax = std::max(vmax, v);
-        if (vmax != 0.0) {
-          std::vector<float> xr((size_t)ne * F);
-          std::vector<uint8_t> olds(ne);
+        std::vector<float> xr((size_t)ne * F);
+        std::vector<uint8_t> olds(ne);
+        if (comm) {
+          // dist.DistComm.farthest: every shard's local top n as (distance,
+          // global row) pairs, all-gathered and ordered by (distance desc, row
+          // asc); the winners' raw rows and old labels all-reduced from their
+          // owners (zeros elsewhere; fp32 values and labels are exact in fp64)
+          std::vector<double> vi(2 * (size_t)ne, -1.0);
+          for (int e = 0; e < m; ++e) {
+            vi[2 * e] = far_v[e];
+            vi[2 * e + 1] = (double)(far_i[e] + comm->row_offset);
+          }
+          MW_HIP(hipMemcpyAsync(comm->d_msg + ML.vi, vi.data(), vi.size() * 8, hipMemcpyHostToDevice, st));
+          MW_HIP(hipStreamSynchronize(st));
+          if ((rc = comm_call(comm->all_gather(comm->ctx, ML.vi, 2 * ne, ML.gathered, stream), "all_gather")) !=
+              MW_OK)
+            break;
+          std::vector<double> gv((size_t)comm->world * 2 * ne);
+          MW_HIP(hipMemcpyAsync(gv.data(), comm->d_msg + ML.gathered, gv.size() * 8, hipMemcpyDeviceToHost, st));
+          MW_HIP(hipStreamSynchronize(st));
+          std::vector<std::pair<double, int64_t>> cand;  // (distance, global row) of every shard
+          for (size_t i = 0; i < gv.size() / 2; ++i)
+            if (gv[2 * i + 1] >= 0) cand.push_back({gv[2 * i], (int64_t)gv[2 * i + 1]});
+          std::sort(cand.begin(), cand.end(), [](const std::pair<double, int64_t>& a,
+                                                 const std::pair<double, int64_t>& b) {
+            return a.first != b.first ? a.first > b.first : a.second < b.second;
+          });
+          cand.resize(std::min<size_t>(cand.size(), (size_t)ne));
+          far_i.assign(ne, 0);
+          far_v.assign(ne, 0.0);
+          for (size_t e = 0; e < cand.size(); ++e) far_v[e] = cand[e].first, far_i[e] = cand[e].second;
+          double vmax = far_v[0];
+          for (double v : far_v) vmax = std::max(vmax, v);
+          std::vector<double> own((size_t)ne * (F + 1), 0.0);
           for (int e = 0; e < ne; ++e) {
-            MW_HIP(hipMemcpyAsync(xr.data() + (size_t)e * F, d_X + far_i[e] * F, F * sizeof(float),
+            const int64_t loc = far_i[e] - comm->row_offset;
+            if (loc < 0 || loc >= S) continue;
+            MW_HIP(hipMemcpyAsync(xr.data() + (size_t)e * F, d_X + loc * F, F * sizeof(float),
                                   hipMemcpyDeviceToHost, st));
-            MW_HIP(hipMemcpyAsync(&olds[e], d_labels[g] + far_i[e], 1, hipMemcpyDeviceToHost, st));
+            MW_HIP(hipMemcpyAsync(&olds[e], d_labels[g] + loc, 1, hipMemcpyDeviceToHost, st));
           }
           MW_HIP(hipStreamSynchronize(st));
+          for (int e = 0; e < ne; ++e) {
+            const int64_t loc = far_i[e] - comm->row_offset;
+            if (loc < 0 || loc >= S) continue;
+            for (int f = 0; f < F; ++f) own[(size_t)e * (F + 1) + f] = (double)xr[(size_t)e * F + f];
+            own[(size_t)e * (F + 1) + F] = (double)olds[e];
+          }
+          MW_HIP(hipMemcpyAsync(comm->d_msg + ML.owners, own.data(), own.size() * 8, hipMemcpyHostToDevice, st));
+          MW_HIP(hipStreamSynchronize(st));
+          if ((rc = comm_call(comm->all_reduce_sum(comm->ctx, ML.owners, (int64_t)own.size(), stream),
+                              "all_reduce_sum")) != MW_OK)
+            break;
+          MW_HIP(hipMemcpyAsync(own.data(), comm->d_msg + ML.owners, own.size() * 8, hipMemcpyDeviceToHost, st));
+          MW_HIP(hipStreamSynchronize(st));
+          if (vmax == 0.0) far_v.clear();  // nothing to move (as _relocate_empty: far_val.max() == 0)
+          for (int e = 0; e < ne; ++e) {
+            for (int f = 0; f < F; ++f) xr[(size_t)e * F + f] = (float)own[(size_t)e * (F + 1) + f];
+            olds[e] = (uint8_t)own[(size_t)e * (F + 1) + F];
+          }
+        } else {
+          double vmax = far_v[0];
+          for (double v : far_v) vmax = std::max(vmax, v);
+          if (vmax == 0.0) {
+            far_v.clear();
+          } else {
+            for (int e = 0; e < ne; ++e) {
+              MW_HIP(hipMemcpyAsync(xr.data() + (size_t)e * F, d_X + far_i[e] * F, F * sizeof(float),
+                                    hipMemcpyDeviceToHost, st));
+              MW_HIP(hipMemcpyAsync(&olds[e], d_labels[g] + far_i[e], 1, hipMemcpyDeviceToHost, st));
+            }
+            MW_HIP(hipStreamSynchronize(st));
+          }
+        }
+        if (!far_v.empty()) {
           for (int e = 0; e < ne; ++e) {
             const uint8_t old = olds[e];
             for (int f = 0; f < F; ++f) {
@@ -1003,10 +1238,7 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
       if (fs.done) MW_HIP(hipMemsetAsync(d_out + roff[g], 0, (size_t)(roff[g + 1] - roff[g]) * 8, st));
     }
   }
-  if (rc != MW_OK) {
-    ev_fail();
-    return rc;
-  }
+  if (rc != MW_OK) return rc;
   for (FitsFit& fs : fits)
     if (!fs.done) fs.n_iter = max_iter;
 
@@ -1039,10 +1271,7 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
     }
   }
   if (rc == MW_OK) rc = download();
-  if (rc != MW_OK) {
-    ev_fail();
-    return rc;
-  }
+  if (rc != MW_OK) return rc;
   size_t c = 0;
   for (int g = 0; g < n; ++g) {
     const FitsFit& fs = fits[g];
@@ -1059,7 +1288,7 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
   }
   if (h_timing) {  // [slot][count, ms, bytes], slots 0..8
     for (int i = 0; i < 27; ++i) h_timing[i] = 0.0;
-    for (Timed& t : timed) {
+    for (TimedLaunches::T& t : timed.v) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, t.a, t.b);
       h_timing[3 * t.slot] += 1.0;
@@ -1067,6 +1296,8 @@ extern "C" int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_
       h_timing[3 * t.slot + 2] += t.bytes;
     }
   }
-  ev_fail();  // (destroys the events)
-  return MW_OK;
+  return MW_OK;  // (the events are destroyed with `timed`)
 }
+
+}  // namespace
+}  // namespace mw

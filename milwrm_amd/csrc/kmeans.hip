@@ -100,11 +100,52 @@ __host__ __device__ inline size_t assign_wave_bytes_xl(int k, int C, int CMAX) {
   const size_t tile = (size_t)64 * C * 4 + (size_t)CMAX * 4, sums = (size_t)(k + 1) * 64 * 12;
   return ((tile > sums ? tile : sums) + 15) & ~(size_t)15;
 }
+// Per-domain confidence sums in fixed point: each confidence (fp32 in [0, 1],
+// or NaN) as the integer rint(conf * 2^32) held in an fp64 (exact), so a
+// lane's sum is an exact integer (< 2^53 while a lane takes < 2^21 pixels), a
+// block's sum an exact uint64, and the records two 32-bit limbs: the domain
+// sums are the same bits however the pixels are split into launches, bands
+// or ranks (np.mean's fp64 sum of the reference, MILWRM.py:447-449, to
+// 2^-33 per pixel).
+constexpr int kDomRec = 3;  // per-block record: [conf hi k | conf lo k | count k]
+__device__ __forceinline__ double conf_fixed(float c) { return (double)rintf(c * 4294967296.f); }
+
+// The per-block record from the waves' lane-private slots (per wave at
+// `slots` + w * wslot: fp64 conf sums [k+1][64] | u32 counts [k+1][64]).
+// A NaN confidence makes its domain's limbs NaN (the reference's mean is NaN).
+__device__ void domain_block_record(const char* slots, size_t wslot, int nw, int k, double* out) {
+  for (int q = threadIdx.x; q < 2 * k; q += blockDim.x) {
+    const int j = q < k ? q : q - k;
+    unsigned long long s = 0;
+    bool nan = false;
+    for (int w = 0; w < nw; ++w) {
+      const double* cs = reinterpret_cast<const double*>(slots + (size_t)w * wslot);
+      const unsigned* cc = reinterpret_cast<const unsigned*>(cs + (k + 1) * 64);
+      for (int l = 0; l < 64; ++l) {
+        if (q < k) {
+          const double v = cs[j * 64 + l];
+          nan |= v != v;
+          s += nan ? 0ull : (unsigned long long)v;
+        } else {
+          s += cc[j * 64 + l];
+        }
+      }
+    }
+    if (q < k) {
+      out[q] = nan ? __builtin_nan("") : (double)(s >> 32);
+      out[k + q] = nan ? __builtin_nan("") : (double)(s & 0xffffffffull);
+    } else {
+      out[k + q] = (double)s;
+    }
+  }
+}
+
 // KMeans.predict + estimate_confidence_score_mxif (MILWRM.py:237-277,
 // 389-450) over every pixel of an HWC image: label of the nearest center
 // (strict argmin, same packed-FMA distance as the Lloyd E-step), confidence
 // (d2 - d1) / d2 from the two smallest distances, -1 / NaN outside the mask.
-// Per-block record: [sum conf k | count k] (fp64, fixed combine order).
+// Per-block record: [conf hi k | conf lo k | count k] (exact fp64 limbs,
+// domain_block_record).
 // Waves stream 64-pixel tiles (64*C floats) with the next tile in flight.
 template <int CMAX, int KS, bool SC, bool XL = false>
 __global__ void __launch_bounds__(256, kAssignWPS) assign_kernel(const float* __restrict__ img, int C,
@@ -228,11 +269,12 @@ __global__ void __launch_bounds__(256, kAssignWPS) assign_kernel(const float* __
       lab_out[p0 + lane] = (int8_t)lab;
       conf_out[p0 + lane] = conf;
     }
-    // per-label sum of confidences and counts: lane-private LDS slots in a
-    // fixed order (pixels outside the mask/tile go to the sink slot k)
+    // per-label sum of confidences and counts: lane-private slots in a fixed
+    // order (pixels outside the mask/tile go to the sink slot k); the
+    // confidences as the integers conf_q (conf_fixed), so every sum is exact
     if constexpr (XL) {  // the same per-slot add sequence, in registers (x + 0.0 == x)
       const int sl = lab < 0 ? k : lab;
-      const double cv = in_mask ? (double)conf : 0.0;
+      const double cv = in_mask ? conf_fixed(conf) : 0.0;
 #pragma unroll
       for (int j = 0; j <= kAssignXLK; ++j) {
         r_cs[j] += sl == j ? cv : 0.0;
@@ -240,7 +282,7 @@ __global__ void __launch_bounds__(256, kAssignWPS) assign_kernel(const float* __
       }
     } else {
       const int slot = (lab < 0 ? k : lab) * 64 + lane;
-      atomicAdd(&w_csum[slot], in_mask ? (double)conf : 0.0);
+      atomicAdd(&w_csum[slot], in_mask ? conf_fixed(conf) : 0.0);
       atomicAdd(&w_ccnt[slot], 1u);
     }
   };
@@ -271,23 +313,7 @@ __global__ void __launch_bounds__(256, kAssignWPS) assign_kernel(const float* __
       }
   }
   __syncthreads();
-  double* out = rec + (size_t)blockIdx.x * 2 * k;
-  for (int q = t; q < 2 * k; q += blockDim.x) {
-    const int j = q < k ? q : q - k;
-    double sacc = 0.0;
-    for (int w = 0; w < nw; ++w) {
-      const double* cs = reinterpret_cast<const double*>(smem + cent_bytes + (size_t)w * wslot);
-      const unsigned* cc = reinterpret_cast<const unsigned*>(cs + (k + 1) * 64);
-      if (q < k) {
-        for (int l = 0; l < 64; ++l) sacc += cs[j * 64 + l];
-      } else {
-        unsigned long long c = 0;
-        for (int l = 0; l < 64; ++l) c += cc[j * 64 + l];
-        sacc += (double)c;
-      }
-    }
-    out[q] = sacc;
-  }
+  domain_block_record(smem + cent_bytes, wslot, nw, k, rec + (size_t)blockIdx.x * kDomRec * k);
 }
 
 // Per-block domain records [sum conf k | count k] from label/confidence maps
@@ -316,27 +342,11 @@ __global__ void __launch_bounds__(256) domain_records_kernel(const int8_t* __res
     const int lb = valid ? (int)lab[p] : -1;
     const float c = valid ? conf[p] : 0.f;
     const int slot = (lb < 0 ? k : lb) * 64 + lane;
-    w_csum[slot] += lb >= 0 ? (double)c : 0.0;
+    w_csum[slot] += lb >= 0 ? conf_fixed(c) : 0.0;
     w_ccnt[slot] += 1u;
   }
   __syncthreads();
-  double* out = rec + (size_t)blockIdx.x * 2 * k;
-  for (int q = t; q < 2 * k; q += blockDim.x) {
-    const int j = q < k ? q : q - k;
-    double sacc = 0.0;
-    for (int w = 0; w < nw; ++w) {
-      const double* cs = reinterpret_cast<const double*>(smem + (size_t)w * wslot);
-      const unsigned* cc = reinterpret_cast<const unsigned*>(cs + (k + 1) * 64);
-      if (q < k) {
-        for (int l = 0; l < 64; ++l) sacc += cs[j * 64 + l];
-      } else {
-        unsigned long long cn = 0;
-        for (int l = 0; l < 64; ++l) cn += cc[j * 64 + l];
-        sacc += (double)cn;
-      }
-    }
-    out[q] = sacc;
-  }
+  domain_block_record(smem, wslot, nw, k, rec + (size_t)blockIdx.x * kDomRec * k);
 }
 
 // waves per assign block (LDS-bound for large k and C): shared with the
@@ -383,9 +393,9 @@ int mw_farthest(const float* d_X, int64_t S, int F, const float* d_a, const floa
   return MW_OK;
 }
 
-// workspace: per-block records [G][2k] fp64 | pair-major centers image
+// workspace: per-block records [G][3k] fp64 | pair-major centers image
 static size_t assign_rec_bytes(int64_t n_pix, int k) {
-  return ((size_t)kblocks(n_pix) * 2 * k * sizeof(double) + 255) & ~(size_t)255;
+  return ((size_t)kblocks(n_pix) * kDomRec * k * sizeof(double) + 255) & ~(size_t)255;
 }
 size_t mw_assign_ws_bytes(int64_t n_pix, int k) {
   return assign_rec_bytes(n_pix, k) + cent_t_bytes(k <= 64 ? 64 : 128, 64) + 256;
@@ -473,8 +483,9 @@ int mw_domain_records(const int8_t* d_label, const float* d_conf, int64_t n_pix,
 
 int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom, void* stream) {
   MW_CHECK_ARG(d_ws && d_dom && k >= 1, "mw_assign_reduce: bad args");
-  hipLaunchKernelGGL(rec_reduce_kernel, dim3((2 * k + 31) / 32), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<const double*>(d_ws), kblocks(n_pix), 2 * k, d_dom);
+  // integer-valued limbs below 2^32 over <= 1024 blocks: the fp64 sums are exact
+  hipLaunchKernelGGL(rec_reduce_kernel, dim3((kDomRec * k + 31) / 32), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const double*>(d_ws), kblocks(n_pix), kDomRec * k, d_dom);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

@@ -31,13 +31,6 @@
 // its own (kD2Blocks row blocks), reduced by lloyd_reduce_fits_kernel.
 #pragma once
 
-// timing variants (tools/probe/d2_variants.sh; wrong results): 1 = no closes,
-// 2 = no key updates, 3 = no queue flushes, 4 = chunk loads + B operands only
-// (no tiles), 5 = chunk loads only
-#ifndef MW_D2_VARIANT
-#define MW_D2_VARIANT 0
-#endif
-
 namespace mw {
 
 constexpr int kD2Tiles = 10;                // MFMA tiles of 32 center slots
@@ -252,12 +245,7 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   int nq_r = 0, nq_m = 0;
   // M-step of the queued changed (row, fit) pairs: two pairs per wave round,
   // lane = feature; four rounds' reads issued before their atomics
-  int sink = 0;
   auto flush_m = [&](int64_t r0) {
-    if (MW_D2_VARIANT == 3) {
-      nq_m = 0;
-      return;
-    }
     const int f = r;  // feature
     for (int e0 = 0; e0 < nq_m; e0 += 8) {
       int v[4];
@@ -291,10 +279,6 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
   // nearest_centers bits: even features in .x, odd in .y, then .x + .y), and
   // the half's 32 lanes reduce to the top two (lowest index on ties)
   auto flush_r = [&](int64_t r0) {
-    if (MW_D2_VARIANT == 3) {
-      nq_r = 0;
-      return;
-    }
     for (int e0 = 0; e0 < nq_r; e0 += 2) {
       const int e = e0 + h;
       const bool ev = e < nq_r;
@@ -452,7 +436,8 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
       const int lab = 32 * tile + (k1 & 31) - o8;
       const float acc1 = __builtin_bit_cast(float, (unsigned)k1 & kD2KeyMask);
       const float acc2 = __builtin_bit_cast(float, (unsigned)k2 & kD2KeyMask);
-      const float eb = kD2BScale * (xx + cmx) + kD2BAbs;
+      // (the row's delta rides in every accumulator: its rounding counts too)
+      const float eb = kD2BScale * (xx + cmx + delta) + kD2BAbs;
       const bool act = valid && fi < nf;
       const bool tie = act && (far || (kf > 1 && !(acc1 - acc2 > 0.5f * eb)));
       const unsigned long long tm = __ballot(tie);
@@ -514,16 +499,6 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
         push(m1, m2, cur - 1);
       }
     };
-    if (MW_D2_VARIANT >= 4) {
-      float sk = xx;
-      if (MW_D2_VARIANT == 4)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) sk += (float)bop[ks][j] + (float)bol[ks][j];
-      sink ^= __builtin_bit_cast(int, sk);
-      continue;
-    }
     for (int tt = 0; tt < ntile; ++tt) {
       const char* ap = s_A + ((size_t)(4 * tt) * 64 + lane) * 16;
       const h8x a0h = *reinterpret_cast<const h8x*>(ap);
@@ -549,7 +524,6 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
           m1 = m2 = KMAX;
         }
         if (fi < 0) continue;
-        if (MW_D2_VARIANT == 2) continue;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v = acc[4 * j + i];  // (a bit_cast of the vector element itself reads element 0)
@@ -575,17 +549,12 @@ __global__ void __launch_bounds__(64 * kD2Waves) lloyd_dense2_kernel(const float
         const int d1 = q == 0 ? pb1[0] : q == 1 ? pb1[1] : pb1[2];
         const int d2 = q == 0 ? pb2[0] : q == 1 ? pb2[1] : pb2[2];
         const int fq = __builtin_amdgcn_readfirstlane(q == 0 ? pf[0] : q == 1 ? pf[1] : pf[2]);
-#if MW_D2_VARIANT == 1
-        sink ^= c1 ^ c2 ^ d1 ^ d2 ^ fq;
-#else
         close2(c1, c2, d1, d2, fq);
-#endif
       }
     }
     flush_r(r0);
     flush_m(r0);
   }
-  if (MW_D2_VARIANT != 0 && sink == 0x5a5a5a5a) s_chg[0] = 1;
   __syncthreads();
   // ---- records: per fit [dQ_hi kF | dQ_lo kF | dcount k | changed | recomputed | 0 | 0] ----
   for (int fi = 0; fi < nf; ++fi) {

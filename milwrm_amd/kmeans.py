@@ -470,7 +470,21 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
     ks = [fs.k for fs in fits]
     rls = [N.query("mw_lloyd_rec_len", k, F) for k in ks]
     roff = np.concatenate([[0], np.cumsum(rls)]).astype(np.int64)
-    out_all = torch.zeros(int(roff[-1]), dtype=torch.float64, device=dev)
+    S_glob, sizes = S, None
+    if comm.sharded():
+        sizes = comm.all_gather_np(np.array([S], dtype=np.int64))[:, 0]
+        S_glob = int(sizes.sum())
+    # the C driver on every rank (the same decision everywhere): one process, or
+    # row shards that all hold rows (mw_lloyd_fits_sharded, the collectives
+    # through _CommHook); the Python loop below otherwise (and for the trace)
+    use_c = USE_C_FITS and TRACE is None and not verbose and (sizes is None or int(sizes.min()) >= 1)
+    msg = None
+    if use_c and sizes is not None:  # the records at the head of the message buffer
+        msg = torch.zeros(N.query("mw_lloyd_fits_msg_len", int(roff[-1]), F, comm.world), dtype=torch.float64,
+                          device=dev)
+        out_all = msg[:int(roff[-1])]
+    else:
+        out_all = torch.zeros(int(roff[-1]), dtype=torch.float64, device=dev)
     outs = [out_all[roff[g]:roff[g + 1]] for g in range(n)]
     plen = [k * F + 2 * k for k in ks]  # per fit: centers | drift | half_sep (fp32)
     poff = np.concatenate([[0], np.cumsum(plen)]).astype(np.int64)
@@ -526,14 +540,13 @@ def lloyd_fits(rows: DeviceRows, inits, max_iter=300, tol=0.0, verbose=False, co
             frac *= min(1.0, fs.drift_max / fs.prev_dmax)
         return KIND_TILE if frac > QUEUE_BELOW else QUEUE_KIND
 
-    S_glob = S
-    if comm.sharded():
-        S_glob = int(comm.all_gather_np(np.array([S], dtype=np.int64))[:, 0].sum())
-
     # lloyd_dense2.h: F <= 30 (kD2MaxK 32); lloyd_dense.h: F <= 64, kDenseMaxFitK = 20
     dense_ok = USE_DENSE and F <= (64 if DENSE_MODE == "1" else 30) and max(ks) <= 20
-    if USE_C_FITS and not comm.sharded() and TRACE is None and not verbose:
-        return _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first, st)
+    if use_c:
+        hook = None
+        if sizes is not None:
+            hook = _CommHook(comm, msg, S_glob, int(sizes[:comm.rank].sum()))
+        return _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first, st, hook)
     for it in range(max_iter):
         active = [g for g in range(n) if not fits[g].done]
         if not active:
@@ -600,9 +613,48 @@ _PASS_NAMES = ["lloyd_pass_mode0_first", "lloyd_pass_mode0_tile", "lloyd_pass_mo
                "lloyd_pass_mode0_dense", "lloyd_pass_mode1", "lloyd_pass_mode2"]
 
 
-def _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first, st):
+FITS_C_USED = {"local": 0, "sharded": 0}  # lloyd_fits calls that ran the C driver (tests)
+
+
+class _CommHook:
+    """``mw_fit_comm`` over a ``dist.DistComm``: the C driver's collectives as
+    the Python loop runs them (``comm.all_reduce_`` of the records, the
+    relocation's all-gather), on slices of the message buffer ``msg`` whose
+    head holds the fits' records."""
+
+    def __init__(self, comm, msg: torch.Tensor, rows_total: int, row_offset: int):
+        self.comm, self.msg, self.err = comm, msg, None
+        self._ar = N.ALL_REDUCE_SUM_FN(self._all_reduce)
+        self._ag = N.ALL_GATHER_FN(self._all_gather)
+        self.struct = N.FitComm(None, comm.world, comm.rank, int(rows_total), int(row_offset), D.P(msg),
+                                msg.numel(), self._ar, self._ag)
+        self.reduces = 0
+
+    def _all_reduce(self, ctx, off, n, stream):
+        try:
+            self.comm.all_reduce_(self.msg[off:off + n])
+            self.reduces += 1
+            return 0
+        except BaseException as e:  # noqa: BLE001  (re-raised after the C call returns)
+            self.err = e
+            return 1
+
+    def _all_gather(self, ctx, in_off, n, out_off, stream):
+        try:
+            g = self.comm.all_gather_t(self.msg[in_off:in_off + n])
+            self.msg[out_off:out_off + self.comm.world * n].copy_(
+                torch.from_numpy(np.ascontiguousarray(g, dtype=np.float64).reshape(-1)))
+            return 0
+        except BaseException as e:  # noqa: BLE001
+            self.err = e
+            return 1
+
+
+def _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first, st, hook=None):
     """lloyd_fits' iterations in mw_lloyd_fits (the same host arithmetic and
-    pass-kind policy in C++: no Python between the passes)."""
+    pass-kind policy in C++: no Python between the passes); over row shards
+    (``hook``) in mw_lloyd_fits_sharded, one all-reduce of the records per
+    pass through the hook."""
     S, F = rows.S, rows.F
     n = len(fits)
     ptrs = lambda ts: (C.c_void_p * n)(*[D.P(t) for t in ts])  # noqa: E731
@@ -621,14 +673,23 @@ def _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first,
     mu = np.ascontiguousarray(rows.mu, dtype=np.float64)
     inv = np.ascontiguousarray(rows.inv, dtype=np.float64)
     nobound = int(os.environ.get("MW_LLOYD_NOBOUND") == "1")
-    N.call("mw_lloyd_fits", D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(rows.qexp_dev),
-           a32.ctypes.data, b32.ctypes.data, qexp.ctypes.data, xmax.ctypes.data, mu.ctypes.data,
-           inv.ctypes.data, n, h_k.ctypes.data, h_init.ctypes.data,
-           ptrs([fs.labels for fs in fits]), ptrs([fs.ub for fs in fits]), ptrs([fs.lb for fs in fits]),
-           ptrs([fs.ws for fs in fits]), D.P(par), D.P(out_all), int(max_iter), float(tol), int(first),
-           int(QUEUE_KIND), float(QUEUE_BELOW), int(DENSE_MIN_FITS) if dense_ok else 0, nobound,
-           centers.ctypes.data, inertia.ctypes.data, n_iter.ctypes.data, hist.ctypes.data, int(max_iter),
-           hist_len.ctypes.data, None if timing is None else timing.ctypes.data, st)
+    args = (D.P(rows.X), S, F, D.P(rows.a32), D.P(rows.b32), D.P(rows.qexp_dev),
+            a32.ctypes.data, b32.ctypes.data, qexp.ctypes.data, xmax.ctypes.data, mu.ctypes.data,
+            inv.ctypes.data, n, h_k.ctypes.data, h_init.ctypes.data,
+            ptrs([fs.labels for fs in fits]), ptrs([fs.ub for fs in fits]), ptrs([fs.lb for fs in fits]),
+            ptrs([fs.ws for fs in fits]), D.P(par), D.P(out_all), int(max_iter), float(tol), int(first),
+            int(QUEUE_KIND), float(QUEUE_BELOW), int(DENSE_MIN_FITS) if dense_ok else -1, nobound,
+            centers.ctypes.data, inertia.ctypes.data, n_iter.ctypes.data, hist.ctypes.data, int(max_iter),
+            hist_len.ctypes.data, None if timing is None else timing.ctypes.data)
+    if hook is None:
+        N.call("mw_lloyd_fits", *args, st)
+        FITS_C_USED["local"] += 1
+    else:
+        status = N.load().mw_lloyd_fits_sharded(*args, C.byref(hook.struct), st)
+        if hook.err is not None:
+            raise hook.err
+        N.check(status, "mw_lloyd_fits_sharded")
+        FITS_C_USED["sharded"] += 1
     if timing is not None:
         for slot, name in enumerate(_PASS_NAMES):
             profiling.add_measured(name, int(timing[3 * slot]), timing[3 * slot + 1], timing[3 * slot + 2])
@@ -745,6 +806,19 @@ def fit_many(rows: DeviceRows, k_values, random_state=None, comm=None, **kw):
             labels = back
         km._set_fitted(rows, labels, inertia, centers, n_iter)
     return models
+
+
+class _Inertia:
+    """The inertia of a fit whose final E-step is still queued: its record in
+    page-locked memory and the event after its copy (mw_kmeans_fit_async)."""
+
+    def __init__(self, event, rec: torch.Tensor, iexp: int):
+        self.event, self.rec, self.iexp = event, rec, int(iexp)
+
+    def value(self) -> float:
+        self.event.synchronize()
+        r = self.rec.numpy()
+        return float((r[-2] * 4294967296.0 + r[-1]) * 2.0 ** -self.iexp)
 
 
 class KMeans:
@@ -870,24 +944,30 @@ class KMeans:
                                  f"match the number of clusters {k} / features {F}.")
         labels = torch.empty(S, dtype=torch.uint8, device=rows.X.device)
         centers = np.zeros((k, F))
-        inertia, n_iter = C.c_double(), C.c_int()
+        n_iter, iexp = C.c_int(), C.c_int()
         idx = np.full(k, -1, dtype=np.int64)
         nb = N.query("mw_kmeans_fit_ws_bytes", S, F, k)
         from .stream import RESIDENCY
 
         RESIDENCY.release(nb + S + (64 << 20))  # workspace + labels; host-backed slide copies go first
         ws = D.WS.get("kfit", nb)
+        # the final E-step's record lands here when the stream gets there: the
+        # fit returns with that pass queued, so whatever the caller queues next
+        # (the label pass) follows it without a host round trip (_Inertia)
+        rec = torch.empty(N.query("mw_lloyd_rec_len", k, F), dtype=torch.float64, pin_memory=True)
         with profiling.timed("kmeans_fit", 0):
-            N.call("mw_kmeans_fit", D.P(rows.X), S, F, mu.ctypes.data, inv.ctypes.data,
+            N.call("mw_kmeans_fit_async", D.P(rows.X), S, F, mu.ctypes.data, inv.ctypes.data,
                    None if var is None else var.ctypes.data,
                    None if xmax is None else xmax.ctypes.data, k,
                    None if c0 is None else c0.ctypes.data,
                    0 if c0 is not None else int(self.random_state),  # unused with an array init
                    int(self.max_iter), float(self.tol or 0.0), D.P(labels), centers.ctypes.data,
-                   C.addressof(inertia), C.addressof(n_iter), idx.ctypes.data, D.P(ws), ws.numel(),
-                   D.stream())
+                   C.addressof(n_iter), idx.ctypes.data, D.P(ws), ws.numel(), rec.data_ptr(),
+                   C.addressof(iexp), D.stream())
+            done = torch.cuda.Event()
+            done.record()
         self.init_indices_ = None if c0 is not None else idx
-        return labels, inertia.value, centers, n_iter.value
+        return labels, _Inertia(done, rec, iexp.value), centers, n_iter.value
 
     def _kpp(self, rows, rs, comm):
         if comm.sharded():
@@ -897,12 +977,24 @@ class KMeans:
     def _set_fitted(self, rows, labels, inertia, centers, n_iter):
         self._labels_dev = labels
         self.cluster_centers_ = centers
-        self.inertia_ = inertia
+        self._inertia = inertia
         self.n_iter_ = n_iter
         self.n_features_in_ = rows.F
         self._n_features_out = int(self.n_clusters)
         self._labels_host = None
         return self
+
+    @property
+    def inertia_(self) -> float:
+        """sklearn's inertia_ (a fit through mw_kmeans_fit_async reads its final
+        record on first access, after the stream has reached it)."""
+        if isinstance(self._inertia, _Inertia):
+            self._inertia = self._inertia.value()
+        return self._inertia
+
+    @inertia_.setter
+    def inertia_(self, v):
+        self._inertia = v
 
     @property
     def labels_(self):

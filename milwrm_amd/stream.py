@@ -426,9 +426,17 @@ def bands(src: RowSource, band_rows: int, halo: int, r0: int = 0, r1=None):
     if nbuf > 1:
         bufs.append(alloc_rows(int(bufs[0].shape[0]), (src.W, src.C), src.dtype, min_rows=lo, dev=dev))
     got = min(int(b.shape[0]) for b in bufs)
-    if got < rows:  # HBM was short: lower bands into the buffers that could be had
+    while got < rows:  # HBM was short: lower bands into the buffers that could be had
+        rows = got
         plan = _plan(H, max(1, got - 2 * halo), halo, r0, r1)
-        nbuf = min(nbuf, len(plan))
+        if len(plan) > 1 and len(bufs) < 2:  # a one-band plan became several: try for a second buffer
+            try:
+                bufs.append(alloc_rows(got, (src.W, src.C), src.dtype, min_rows=min(got, lo), dev=dev))
+            except torch.OutOfMemoryError:
+                pass  # one buffer: each read waits until the band before it is consumed
+        bufs = bufs[:max(1, min(2, len(plan)))]
+        got = min(int(b.shape[0]) for b in bufs)
+    nbuf = len(bufs)
     side = _side_stream(dev)
     main = torch.cuda.current_stream()
     ready = [None] * nbuf
@@ -450,7 +458,7 @@ def bands(src: RowSource, band_rows: int, halo: int, r0: int = 0, r1=None):
     try:
         issue(0)
         for i, (y0, y1, a, b) in enumerate(plan):
-            if i + 1 < len(plan):
+            if nbuf > 1 and i + 1 < len(plan):  # the next band into the other buffer, now
                 issue(i + 1)
             s = i % nbuf
             main.wait_event(ready[s])
@@ -458,6 +466,8 @@ def bands(src: RowSource, band_rows: int, halo: int, r0: int = 0, r1=None):
             ev = torch.cuda.Event()
             ev.record(main)
             free[s] = ev
+            if nbuf == 1 and i + 1 < len(plan):  # one buffer: after this band's consumers
+                issue(i + 1)
     finally:
         main.wait_stream(side)
 

@@ -35,7 +35,9 @@ def _slides():
 
 def _run(slides, batches, comm):
     import milwrm_amd as M
+    from milwrm_amd import kmeans as KM
 
+    used = dict(KM.FITS_C_USED)
     imgs = [M.img(r.copy(), mask=m.copy()) for r, m in slides]
     ests, pix = zip(*[im.calculate_non_zero_mean() for im in imgs])
     df = pd.DataFrame({"Img": imgs, "batch_names": batches, "mean estimators": list(ests),
@@ -53,6 +55,7 @@ def _run(slides, batches, comm):
     lab.find_optimal_k(random_state=18, alpha=0.05)
     out["best_k"] = int(lab.k)
     out["curve"] = lab.inertia_curve_["Scaled Inertia"].values
+    out["fits_c"] = {key: KM.FITS_C_USED[key] - used[key] for key in used}
     return out
 
 
@@ -66,10 +69,19 @@ def _worker(rank, world, port, q):
         torch.cuda.set_device(0)
         from milwrm_amd.dist import DistComm
 
+        from milwrm_amd import kmeans as KM
+
         slides = _slides()
         mine = SHARDS[rank]
         res = _run([slides[i] for i in mine], [BATCHES[i] for i in mine],
                    DistComm(device=torch.device("cpu")))
+        # the same run with the sharded fits in the Python loop (MW_LLOYD_FITS_C=0)
+        KM.USE_C_FITS = False
+        try:
+            res["pyloop"] = _run([slides[i] for i in mine], [BATCHES[i] for i in mine],
+                                 DistComm(device=torch.device("cpu")))
+        finally:
+            KM.USE_C_FITS = True
         torch.cuda.synchronize()
         q.put((rank, res))
     except Exception as e:  # surface the failure in the parent
@@ -112,6 +124,20 @@ def test_two_shards_bitwise_equal_single_process(gpu):
     # clustering rows: rank order = image order
     np.testing.assert_array_equal(np.concatenate([got[0]["rows_labels"], got[1]["rows_labels"]]),
                                   ref["rows_labels"])
+    for r in (0, 1):
+        # the sharded fit (k = 6) and the sweep ran in the C driver
+        # (mw_lloyd_fits_sharded), the single process in mw_kmeans_fit /
+        # mw_lloyd_fits; the Python loop over the same shards gives the same bits
+        g = got[r]
+        assert g["fits_c"]["sharded"] >= 2 and g["fits_c"]["local"] == 0, g["fits_c"]
+        py = g["pyloop"]
+        assert py["fits_c"]["sharded"] == 0, py["fits_c"]
+        for key in ("idx", "centers", "curve", "rows_labels"):
+            np.testing.assert_array_equal(py[key], g[key], err_msg=f"python loop vs C: {key}")
+        assert py["n_iter"] == g["n_iter"] and py["inertia"] == g["inertia"] and py["best_k"] == g["best_k"]
+        for j in range(len(SHARDS[r])):
+            np.testing.assert_array_equal(py["tid"][j], g["tid"][j])
+            np.testing.assert_array_equal(py["cid"][j], g["cid"][j])
 
 
 def _band_worker(rank, world, port, q):

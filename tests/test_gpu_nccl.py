@@ -103,10 +103,15 @@ def _worker(port, q):
         from milwrm_amd import device as D
         from milwrm_amd.dist import LOCAL_COMM, DistComm
 
+        from milwrm_amd import kmeans as KM
+
         comm = DistComm(force=True)
         assert comm.device.type == "cuda" and comm.sharded()
-        res = {"local": _run_slides(LOCAL_COMM), "nccl": _run_slides(comm),
-               "band_local": _run_band(None), "band_nccl": _run_band(comm)}
+        res = {"local": _run_slides(LOCAL_COMM)}
+        used = dict(KM.FITS_C_USED)
+        res["nccl"] = _run_slides(comm)  # the fits in mw_lloyd_fits_sharded, records all-reduced by RCCL
+        res["fits_c"] = {key: KM.FITS_C_USED[key] - used[key] for key in used}
+        res.update(band_local=_run_band(None), band_nccl=_run_band(comm))
         before = dict(D.FUSED_USED)
         os.environ["MW_FUSED_BLUR"] = "1"
         res["band_fused"] = _run_band(comm)
@@ -141,6 +146,7 @@ def test_rccl_message_path_bitwise_equal_local(gpu):
     assert not isinstance(res, str), res
     assert p.exitcode == 0
     _equal(res["local"], res["nccl"], "whole slides, nccl vs local")
+    assert res["fits_c"]["sharded"] >= 2 and res["fits_c"]["local"] == 0, res["fits_c"]
     _equal(res["band_local"], res["band_nccl"], "one band, nccl vs local")
     _equal(res["band_local"], res["band_fused"], "one band with deferred blur vs local")
     # the deferred band really took the fused sample epilogue and the banded label pass

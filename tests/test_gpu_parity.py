@@ -425,12 +425,18 @@ def test_large_properties(gpu):
     cid = (srt[:, 1] - srt[:, 0]) / srt[:, 1]
     _labels_match(L[ys, xs][sel], ref, cid)
     np.testing.assert_allclose(Cf[ys, xs][sel], cid, rtol=RTOL, atol=RTOL)
-    # per-domain sums are the sums of the per-pixel outputs
+    # per-domain sums are the sums of the per-pixel outputs: exactly the sum of
+    # the fixed-point confidences rint(conf * 2^32), split in two 32-bit limbs
+    from milwrm_amd.assign import dom_sums
+
     dm = dom.cpu().numpy()
+    s, cnt = dom_sums(dm, 8)
     for j in range(8):
         sel_j = L == j
-        assert dm[8 + j] == sel_j.sum()
-        np.testing.assert_allclose(dm[j], np.nansum(Cf[sel_j].astype(np.float64)), rtol=1e-6)
+        assert cnt[j] == sel_j.sum()
+        q = np.rint(Cf[sel_j].astype(np.float64) * 2.0 ** 32).astype(np.uint64).sum(dtype=np.uint64)
+        assert dm[j] == float(int(q) >> 32) and dm[8 + j] == float(int(q) & 0xFFFFFFFF)
+        np.testing.assert_allclose(s[j], np.nansum(Cf[sel_j].astype(np.float64)), rtol=1e-9)
 
 
 def test_device_mt19937_subsample_indices_bit_exact(gpu):
