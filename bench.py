@@ -420,7 +420,8 @@ def main():
         print("bench.py: --gpus must be >= 1", file=sys.stderr)
         sys.exit(2)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        check_devices(args.gpus)  # before any GPU call
+        if os.environ.get("MW_BENCH_SHARE_GPU") != "1":
+            check_devices(args.gpus)  # before any GPU call
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and "--gpus" in " ".join(sys.argv):
@@ -428,10 +429,20 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MW_BENCH_SHARE_GPU=1 with MW_BENCH_BACKEND=gloo: every rank on cuda:0 and
+    # the messages over gloo (the multi-rank host path rehearsed on one GPU;
+    # RCCL needs one GPU per rank)
+    share = os.environ.get("MW_BENCH_SHARE_GPU") == "1"
+    backend = os.environ.get("MW_BENCH_BACKEND", "nccl")
+    if share:
+        local = 0
     check_devices(local + 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from milwrm_amd import device as D
     from milwrm_amd import profiling
     from milwrm_amd.dist import make_comm
@@ -481,7 +492,7 @@ def main():
               file=sys.stderr, flush=True)
     profiling.enable(False)
     prof = profiling.summary()
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -550,6 +561,15 @@ def main():
         S_glob = S * world
         out["metric"] = ("pixels/sec (node) through find_optimal_k (k=2..20 sweep, inertia curve) over "
                          "the prepped rows of 30-ch MxIF slides")
+        hostp = prof.get("lloyd_fits_host", {})
+        commp = prof.get("lloyd_fits_comm", {})
+        out["sweep_driver"] = {
+            "iterations": int(hostp.get("count", 0)) // max(args.steps, 1),
+            "host_ms_per_iteration": hostp.get("total_ms", 0.0) / max(hostp.get("count", 0), 1),
+            "comm_ms_per_iteration": commp.get("total_ms", 0.0) / max(commp.get("count", 0), 1) if commp else 0.0,
+            "backend": dist.get_backend() if world > 1 else None,
+            "note": "mw_lloyd_fits(_sharded): host time from a pass's records arriving to the next pass "
+                    "queued, and time inside the all-reduce callback (sharded runs)"}
         out["sweep"] = {"seconds": ms / 1e3, "best_k": int(lab.k), "rows_total": S_glob,
                         "n_iter": {int(a): int(b) for a, b in iters.items()},
                         "fit_passes": fit_passes, "lloyd_device_ms": pass_ms,

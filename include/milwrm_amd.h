@@ -375,8 +375,10 @@ int mw_kmeans_fit_async(const float* d_X, int64_t S, int F, const double* h_mu,
  * while >= dense_min fits run (< 0: never), nobound != 0: no bound ever holds.
  * Outputs: h_centers (the fits' k x F fp64 blocks), h_inertia[n],
  * h_n_iter[n]; h_hist (may be NULL): per fit hist_cap x (changed, recomputed)
- * int64, h_hist_len[n] entries; h_timing (may be NULL): 9 x (launches, ms,
- * algorithmic bytes) of the passes by mode-0 kind 0..6, mode 1, mode 2.
+ * int64, h_hist_len[n] entries; h_timing (may be NULL, 30 doubles): 9 x
+ * (launches, ms, algorithmic bytes) of the passes by mode-0 kind 0..6, mode 1,
+ * mode 2, then (host intervals, their host ms: from a pass's records arriving
+ * to the next pass queued, ms inside the caller's collectives).
  * Synchronises `stream`. */
 int mw_lloyd_fits(const float* d_X, int64_t S, int F, const float* d_a32, const float* d_b32,
                   const int32_t* d_qexp, const float* h_a32, const float* h_b32,
@@ -448,7 +450,7 @@ int mw_farthest(const float* d_X, int64_t S, int F, const float* d_a,
  * mask == 0 → label -1, conf NaN.  Per-block records per label go to d_ws,
  * mw_assign_reduce folds them into d_dom (fp64 [3k]) = [conf hi k | conf lo k
  * | count k]: the per-domain sum of the confidences in exact fixed point,
- * sum of rint(conf * 2^32) = hi * 2^32 + lo (value = that * 2^-32; NaN limbs
+ * sum of rint(conf * 2^32) = hi * 2^32 + lo, 0 <= lo < 2^32 (value = that * 2^-32; NaN limbs
  * when a confidence of the domain is NaN), and the pixel counts.  Every entry
  * is an integer-valued fp64 below 2^53, so records of several launches (row
  * bands, ranks) add exactly: the domain sums do not depend on how the pixels

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -1021,11 +1022,34 @@ int lloyd_fits_impl(const float* d_X, int64_t S, int F, const float* d_a32, cons
   };
   // one all-reduce of the exact records over the shards (the only exchange of
   // a pass), then one download
+  // host time per iteration (h_timing): from a record's arrival to the next
+  // pass queued, and inside the caller's collectives
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) {
+    return std::chrono::duration<double, std::milli>(clk::now() - a).count();
+  };
+  double host_ms = 0.0, comm_ms = 0.0;
+  int host_n = 0;
+  clk::time_point t_ready{};
+  bool have_ready = false;
   auto download = [&]() -> int {
-    if (comm) MW_TRY(comm_call(comm->all_reduce_sum(comm->ctx, 0, roff[n], stream), "all_reduce_sum"));
+    if (comm) {
+      const clk::time_point t0 = clk::now();
+      MW_TRY(comm_call(comm->all_reduce_sum(comm->ctx, 0, roff[n], stream), "all_reduce_sum"));
+      comm_ms += ms_since(t0);
+    }
     MW_HIP(hipMemcpyAsync(rec, d_out, rec_bytes, hipMemcpyDeviceToHost, st));
     MW_HIP(hipStreamSynchronize(st));
+    t_ready = clk::now();
+    have_ready = true;
     return MW_OK;
+  };
+  auto host_mark = [&]() {  // the next pass is about to be queued
+    if (have_ready) {
+      host_ms += ms_since(t_ready);
+      ++host_n;
+      have_ready = false;
+    }
   };
   const MsgLayout ML = msg_layout(roff[n], F, comm ? comm->world : 1);
   if (comm) MW_CHECK_ARG(comm->msg_len >= ML.total, "mw_lloyd_fits_sharded: msg_len %lld < %lld",
@@ -1066,6 +1090,7 @@ int lloyd_fits_impl(const float* d_X, int64_t S, int F, const float* d_a32, cons
       }
       by_kind[kind].push_back(g);
     }
+    host_mark();
     for (int kind = 0; kind < 8 && rc == MW_OK; ++kind)
       if (!by_kind[kind].empty()) rc = launch(by_kind[kind], 0, kind);
     if (rc != MW_OK || (rc = download()) != MW_OK) break;
@@ -1263,6 +1288,7 @@ int lloyd_fits_impl(const float* d_X, int64_t S, int F, const float* d_a32, cons
     fs.iexp = exp_below(xc * xc * 1.01);
   }
   if ((rc = upload(all)) == MW_OK) {
+    host_mark();
     for (int mode = 1; mode <= 2 && rc == MW_OK; ++mode) {
       std::vector<int> sel;
       for (int g = 0; g < n; ++g)
@@ -1286,8 +1312,11 @@ int lloyd_fits_impl(const float* d_X, int64_t S, int F, const float* d_a32, cons
       h_hist_len[g] = m;
     }
   }
-  if (h_timing) {  // [slot][count, ms, bytes], slots 0..8
+  if (h_timing) {  // [slot][count, ms, bytes], slots 0..8; then host intervals, host ms, comm ms
     for (int i = 0; i < 27; ++i) h_timing[i] = 0.0;
+    h_timing[27] = host_n;
+    h_timing[28] = host_ms;
+    h_timing[29] = comm_ms;
     for (TimedLaunches::T& t : timed.v) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, t.a, t.b);

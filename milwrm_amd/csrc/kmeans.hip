@@ -140,6 +140,15 @@ __device__ void domain_block_record(const char* slots, size_t wslot, int nw, int
   }
 }
 
+// canonical limbs of the reduced domain records: lo in [0, 2^32) (NaN stays NaN)
+__global__ void dom_carry_kernel(double* __restrict__ dom, int k) {
+  for (int j = threadIdx.x; j < k; j += blockDim.x) {
+    const double c = floor(dom[k + j] * (1.0 / 4294967296.0));  // exact: power-of-two scale
+    dom[j] += c;
+    dom[k + j] -= c * 4294967296.0;
+  }
+}
+
 // KMeans.predict + estimate_confidence_score_mxif (MILWRM.py:237-277,
 // 389-450) over every pixel of an HWC image: label of the nearest center
 // (strict argmin, same packed-FMA distance as the Lloyd E-step), confidence
@@ -483,9 +492,11 @@ int mw_domain_records(const int8_t* d_label, const float* d_conf, int64_t n_pix,
 
 int mw_assign_reduce(const void* d_ws, int64_t n_pix, int k, double* d_dom, void* stream) {
   MW_CHECK_ARG(d_ws && d_dom && k >= 1, "mw_assign_reduce: bad args");
-  // integer-valued limbs below 2^32 over <= 1024 blocks: the fp64 sums are exact
+  // integer-valued limbs below 2^32 over <= 1024 blocks: the fp64 sums are exact;
+  // then the lo limbs' carries into the hi limbs (one canonical form: lo < 2^32)
   hipLaunchKernelGGL(rec_reduce_kernel, dim3((kDomRec * k + 31) / 32), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const double*>(d_ws), kblocks(n_pix), kDomRec * k, d_dom);
+  hipLaunchKernelGGL(dom_carry_kernel, dim3(1), dim3(128), 0, as_stream(stream), d_dom, k);
   MW_LAUNCH_CHECK();
   return MW_OK;
 }

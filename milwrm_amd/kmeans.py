@@ -665,7 +665,7 @@ def _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first,
     n_iter = np.empty(n, dtype=np.int32)
     hist = np.zeros((n, max_iter, 2), dtype=np.int64)
     hist_len = np.zeros(n, dtype=np.int32)
-    timing = np.zeros(27, dtype=np.float64) if profiling.enabled() else None
+    timing = np.zeros(30, dtype=np.float64) if profiling.enabled() else None
     a32 = np.ascontiguousarray(rows.a_host, dtype=np.float32)
     b32 = np.ascontiguousarray(rows.b_host, dtype=np.float32)
     qexp = np.ascontiguousarray(rows.qexp, dtype=np.int32)
@@ -693,6 +693,10 @@ def _lloyd_fits_c(rows, fits, rls, out_all, par, max_iter, tol, dense_ok, first,
     if timing is not None:
         for slot, name in enumerate(_PASS_NAMES):
             profiling.add_measured(name, int(timing[3 * slot]), timing[3 * slot + 1], timing[3 * slot + 2])
+        # host time between passes (no device work): per-iteration overhead of the driver
+        profiling.add_measured("lloyd_fits_host", int(timing[27]), timing[28], 0)
+        if hook is not None:
+            profiling.add_measured("lloyd_fits_comm", int(timing[27]), timing[29], 0)
     res = []
     o = 0
     for g, fs in enumerate(fits):
