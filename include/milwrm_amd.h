@@ -241,6 +241,30 @@ int mw_kpp_step(const float* d_X, int64_t S, int F, const double* d_mu,
 /* single-device: chosen indices (int64 [k]) into d_idx_out */
 int mw_kpp_indices(const void* d_ws, int64_t S, int T, int k, int64_t* d_idx_out,
                    void* stream);
+/* single-device last step (c = k-1 >= 2, mw_kpp_fold_supported) with the
+ * first Lloyd E-step folded into its pass (the fit driver's default; no
+ * reference counterpart: it replaces the pass over the rows that sklearn's
+ * first lloyd_iter_chunked_dense makes after _kmeans_plusplus, _kmeans.py:
+ * 624-752): besides the step's trial sums, every row gets its label among the
+ * k-1 centers so far (labels), distance bounds valid whichever candidate wins
+ * (ub, lb), the bits "moves to the new center if candidate t wins" (moved,
+ * S bytes) and the base cluster sums as Lloyd block records (d_rec,
+ * mw_kpp_fold_rec_bytes) folded into d_rec_out (mw_lloyd_rec_len(k, F) fp64).
+ * first = the first center's row; d_a32 / d_b32 / d_qexp as mw_lloyd_pass;
+ * d_centers_img = 8 KB of device scratch.  After mw_kpp_indices, the winner's
+ * moved rows are listed (mw_lloyd_list_moved) and a mode-0 mw_lloyd_pass of
+ * kind 8 over the k final centers moves them: its record plus d_rec_out's
+ * sums and counts are those of a kind-0 first pass, bit for bit. */
+int mw_kpp_step_fold(const float* d_X, int64_t S, int F, const double* d_mu, const double* d_inv, int c,
+                     const double* h_u, int T, void* d_ws, int64_t first, const float* d_a32,
+                     const float* d_b32, const int32_t* d_qexp, uint8_t* d_labels, float* d_ub, float* d_lb,
+                     uint8_t* d_moved, void* d_centers_img, double* d_rec, double* d_rec_out, void* stream);
+size_t mw_kpp_fold_rec_bytes(int64_t S, int k, int F);
+/* 1 when mw_kpp_step_fold takes (k, F, T): 3 <= k <= 16, T <= 4, F <= 32 and
+ * its LDS fits four blocks per CU */
+int mw_kpp_fold_supported(int k, int F, int T);
+/* device address of the k-means++ workspace's selected-array index (int) */
+const int* mw_kpp_best_ptr(const void* d_ws, int64_t S, int T);
 /* sharded: local potentials (fp64) of the arrays finished before step c
  * (1 array after init, T after a trial) */
 int mw_kpp_pots(const void* d_ws, int64_t S, int T, int c, double* d_pots, void* stream);
@@ -307,6 +331,10 @@ size_t mw_lloyd_ws_bytes(int64_t S, int k, int F);
  * is 0 or S >= 2^31 (kind 4 falls back to kind 2 there): a fit whose passes
  * never take kind 4 (MW_LLOYD_LIST=0) needs only its per-block records. */
 size_t mw_lloyd_ws_bytes_kinds(int64_t S, int k, int F, int with_list);
+/* kind 8 = kind 4 over row lists written beforehand into ws: the rows of
+ * d_moved (mw_kpp_step_fold) whose bit *d_best is set (S < 2^31) */
+int mw_lloyd_list_moved(const uint8_t* d_moved, const int* d_best, int64_t S, int F, int k, void* d_ws,
+                        void* stream);
 int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
                   const int32_t* d_qexp, int n, const mw_lloyd_fit* h_fits, int mode, int kind,
                   void* stream);

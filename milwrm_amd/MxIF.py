@@ -643,8 +643,12 @@ class img:
                 means = s / c
             return [float(m) * pixels for m in means], pixels
         s, c = self._nz_stats()
-        self._prefetch_mask_rank()  # queued behind nz_stats, overlaps the host work that follows
-        s, c = D.d2h(s, c)
+        pending = D.d2h_async(s, c)
+        # the mask rank queued behind the copies: it runs while the host waits
+        # for them and does the work that follows (the blur needs its result
+        # only later), instead of before them
+        self._prefetch_mask_rank()
+        s, c = pending.wait()
         pixels = int(c.sum())
         with np.errstate(invalid="ignore", divide="ignore"):
             means = s / c

@@ -58,11 +58,17 @@ _PROTOS = {
     "mw_kpp_init": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp]),
     "mw_kpp_step": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_kpp_indices": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "mw_kpp_step_fold": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_i64, c_vp, c_vp,
+                                 c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mw_kpp_fold_rec_bytes": (c_sz, [c_i64, c_i32, c_i32]),
+    "mw_kpp_fold_supported": (c_i32, [c_i32, c_i32, c_i32]),
+    "mw_kpp_best_ptr": (c_vp, [c_vp, c_i64, c_i32]),
     "mw_kpp_pots": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mw_kpp_search": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "mw_kpp_trial": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "mw_lloyd_ws_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "mw_lloyd_ws_bytes_kinds": (c_sz, [c_i64, c_i32, c_i32, c_i32]),
+    "mw_lloyd_list_moved": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mw_lloyd_rec_len": (c_i32, [c_i32, c_i32]),
     "mw_lloyd_pass": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "mw_col_absmax": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),

@@ -78,6 +78,46 @@ __device__ __forceinline__ double wave_sum_lane0(double v) {
   return v;
 }
 
+// v_permlane32_swap / v_permlane16_swap of a double pair (two dwords each):
+// x32 exchanges the upper 32 lanes of `a` with the lower 32 lanes of `b`; x16
+// the odd 16-lane rows of `a` with the even rows of `b`
+__device__ __forceinline__ void pl_swap_d(double& a, double& b, bool x16) {
+  const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+  const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+  unsigned a0 = (unsigned)ua, a1 = (unsigned)(ua >> 32), b0 = (unsigned)ub, b1 = (unsigned)(ub >> 32);
+  if (x16) {
+    const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+    a0 = r0[0]; b0 = r0[1]; a1 = r1[0]; b1 = r1[1];
+  } else {
+    const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    a0 = r0[0]; b0 = r0[1]; a1 = r1[0]; b1 = r1[1];
+  }
+  a = __longlong_as_double((long long)(((unsigned long long)a1 << 32) | a0));
+  b = __longlong_as_double((long long)(((unsigned long long)b1 << 32) | b0));
+}
+
+// wave_sum_lane0 of four values at once: v_r's sum lands in lane 16 r, bit
+// for bit wave_sum_lane0(v_r)'s lane 0.  The l ^ 32 and l ^ 16 levels
+// exchange register halves instead of LDS permutes, and each lane goes on
+// with the one value its row keeps (lower half: v0, v1, upper: v2, v3; then
+// row r: v_r): every level adds the same lane pairs as wave_sum_lane0's
+// tree, so lane 16 r ends with lane 0's additions for v_r, in the same order
+// (rows of 16 lanes then reduce by the same DPP row shifts)
+__device__ __forceinline__ double wave_sum4_rows(double v0, double v1, double v2, double v3) {
+  pl_swap_d(v0, v2, false);  // lower lanes: (own v0, v0 of l + 32); upper: (v2 of l - 32, own v2)
+  pl_swap_d(v1, v3, false);
+  double p = v0 + v2, q = v1 + v3;  // lower: v0, v1 pair sums; upper: v2, v3
+  pl_swap_d(p, q, true);            // row 0: (p, p of l + 16); 1: (q of l - 16, q); 2, 3 likewise
+  double v = p + q;
+  v += dpp_row_shl<8>(v);
+  v += dpp_row_shl<4>(v);
+  v += dpp_row_shl<2>(v);
+  v += dpp_row_shl<1>(v);
+  return v;
+}
+
 // Block-wide sum of one value per thread; result valid in thread 0.
 // `scratch` must hold blockDim.x/64 elements.  Fixed combine order.
 template <typename T>

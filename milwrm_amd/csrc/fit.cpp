@@ -264,7 +264,10 @@ struct Fit {
     return MW_OK;
   }
 
-  int pass(int mode, int kind, int iexp, std::vector<double>& rec) {
+  // fold_rec: the first pass of a k-means++ fold (kind 8): the record is the
+  // list pass's moves plus the fold pass's base sums (out + rl), with the fold
+  // record's counters (every row changed from unlabelled and was computed)
+  int pass(int mode, int kind, int iexp, std::vector<double>& rec, bool fold_rec = false) {
     mw_lloyd_fit f{};
     f.centers = par;
     f.drift = par + (size_t)k * F;
@@ -278,15 +281,22 @@ struct Fit {
     f.drift_max = drift_max;
     f.inertia_exp = iexp;
     MW_TRY(mw_lloyd_pass(X, S, F, a32, b32, qexp, 1, &f, mode, kind, st));
-    rec.resize(rl);
+    const int nr = fold_rec ? 2 * rl : rl;
+    rec.resize(nr);
     char* pin = pinned_staging();
-    if (pin && (size_t)rl * sizeof(double) <= kPinRows - kPinRec) {
-      MW_HIP(hipMemcpyAsync(pin + kPinRec, out, rl * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (pin && (size_t)nr * sizeof(double) <= kPinRows - kPinRec) {
+      MW_HIP(hipMemcpyAsync(pin + kPinRec, out, nr * sizeof(double), hipMemcpyDeviceToHost, st));
       MW_HIP(hipStreamSynchronize(st));
-      std::memcpy(rec.data(), pin + kPinRec, rl * sizeof(double));
+      std::memcpy(rec.data(), pin + kPinRec, nr * sizeof(double));
     } else {
-      MW_HIP(hipMemcpyAsync(rec.data(), out, rl * sizeof(double), hipMemcpyDeviceToHost, st));
+      MW_HIP(hipMemcpyAsync(rec.data(), out, nr * sizeof(double), hipMemcpyDeviceToHost, st));
       MW_HIP(hipStreamSynchronize(st));
+    }
+    if (fold_rec) {  // integer-valued limbs and counts: exact fp64 sums
+      const int ns = 2 * k * F + k;
+      for (int i = 0; i < ns; ++i) rec[i] += rec[rl + i];
+      for (int i = ns; i < rl; ++i) rec[i] = rec[rl + i];
+      rec.resize(rl);
     }
     return MW_OK;
   }
@@ -355,7 +365,7 @@ struct Fit {
 // records | out | one region shared by the column statistics (tolerance),
 // the k-means++ state and the relocation scratch (never live together).
 struct FitLayout {
-  size_t small, par, ub, lb, lws, out, big, total;
+  size_t small, par, ub, lb, lws, out, big, fold, total;
 };
 static inline size_t fal(size_t x) { return (x + 255) & ~(size_t)255; }
 static int lloyd_queue_kind() {  // MW_LLOYD_LIST=0: one-kernel kQueue (A/B)
@@ -373,12 +383,15 @@ static FitLayout fit_layout(int64_t S, int F, int k) {
   L.ub = L.par + fal(((size_t)k * F + 2 * k) * 4);
   L.lb = L.ub + fal((size_t)S * 4);
   L.lws = L.lb + fal((size_t)S * 4);
-  L.out = L.lws + fal(mw_lloyd_ws_bytes_kinds(S, k, F, lloyd_queue_kind() == 4));
-  L.big = L.out + fal((size_t)mw_lloyd_rec_len(k, F) * 8);
+  // the records of a k-means++ fold pass (kpp grid) share the Lloyd records' region
+  L.out = L.lws + fal(std::max(mw_lloyd_ws_bytes_kinds(S, k, F, lloyd_queue_kind() == 4),
+                               mw_kpp_fold_rec_bytes(S, k, F)));
+  L.big = L.out + fal((size_t)2 * mw_lloyd_rec_len(k, F) * 8);  // pass record | fold record
   size_t big = mw_gather_ws_bytes(S, F);
   if (T <= 8) big = std::max(big, mw_kpp_ws_bytes(S, T));
   big = std::max(big, mw_farthest_ws_bytes(S));
-  L.total = L.big + fal(big);
+  L.fold = L.big + fal(big);  // fold: center image (8 KB) | moved bits (S bytes)
+  L.total = L.fold + fal(8192) + fal((size_t)S);
   return L;
 }
 
@@ -473,6 +486,20 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
   fit.out = reinterpret_cast<double*>(base + L.out);
   void* big = base + L.big;
   fit.labels = d_labels;
+  // MW_KPP_FOLD=1: the first Lloyd E-step folded into the last k-means++
+  // pass (kpp.hip mw_kpp_step_fold) for a seeded k-means++ init
+  // (mw_kpp_fold_supported: 3 <= k <= 16, T <= 4, F <= 32) with kList passes.
+  // Same bits as the separate first pass (tests/test_gpu_fit_c.py); not the
+  // default: the fused pass (1.15 ms at config 2) costs what the two passes
+  // it replaces do (0.49 + 0.77 ms) and the moved rows' list pass comes on
+  // top
+  const bool fold_env = [] {  // read per fit (tests compare both forms in one process)
+    const char* e = getenv("MW_KPP_FOLD");
+    return e && e[0] == '1';
+  }();
+  const bool fold = fold_env && !h_init && mw_kpp_fold_supported(k, F, T) && S < ((int64_t)1 << 31) &&
+                    lloyd_queue_kind() == 4;
+  uint8_t* d_moved = reinterpret_cast<uint8_t*>(base + L.fold + 8192);
 
   // folded scaler: x' = x * a + b (fp32), as DeviceRows
   std::vector<float> a32(F), b32(F);
@@ -553,7 +580,12 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
     std::vector<double> u(T);
     for (int c = 1; c < k; ++c) {
       for (int t = 0; t < T; ++t) u[t] = rs.sample();
-      MW_TRY(mw_kpp_step(d_X, S, F, d_mu, d_inv, c, u.data(), T, big, st));
+      if (fold && c == k - 1)
+        MW_TRY(mw_kpp_step_fold(d_X, S, F, d_mu, d_inv, c, u.data(), T, big, first, fit.a32, fit.b32, fit.qexp,
+                                d_labels, fit.ub, fit.lb, d_moved, base + L.fold, reinterpret_cast<double*>(fit.ws),
+                                fit.out + fit.rl, st));
+      else
+        MW_TRY(mw_kpp_step(d_X, S, F, d_mu, d_inv, c, u.data(), T, big, st));
     }
     MW_TRY(mw_kpp_indices(big, S, T, k, d_idx, st));
     std::vector<int64_t> idx(k);
@@ -569,8 +601,8 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
     }
   }
 
-  // Lloyd iterations
-  MW_HIP(hipMemsetAsync(d_labels, 255, (size_t)S, st));
+  // Lloyd iterations (the fold pass labelled every row already)
+  if (!fold) MW_HIP(hipMemsetAsync(d_labels, 255, (size_t)S, st));
   std::vector<int64_t> q_hi((size_t)k * F, 0), q_lo((size_t)k * F, 0), count(k, 0);
   std::vector<double> rec, cnew((size_t)k * F), weight(k), tmp(std::max(F, k));
   int64_t last_recomputed = -1;
@@ -594,7 +626,14 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
         frac *= std::min(1.0, (double)fit.drift_max / (double)fit.prev_dmax);
       kind = frac > queue_below ? 1 : queue_kind;
     }
-    MW_TRY(fit.pass(0, kind, 0, rec));
+    if (fold && it == 0) {
+      // the k-means++ fold: the winner's moved rows, listed, then recomputed
+      // against the k final centers (kind 8) -- the first pass's record
+      MW_TRY(mw_lloyd_list_moved(d_moved, mw_kpp_best_ptr(big, S, T), S, F, k, fit.ws, st));
+      MW_TRY(fit.pass(0, 8, 0, rec, true));
+    } else {
+      MW_TRY(fit.pass(0, kind, 0, rec));
+    }
     for (size_t i = 0; i < (size_t)k * F; ++i) {
       q_hi[i] += (int64_t)rec[i];
       q_lo[i] += (int64_t)rec[(size_t)k * F + i];

@@ -36,6 +36,31 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 __host__ __device__ constexpr int kpad4(int k) { return (k + 3) & ~3; }
 
+// Lloyd per-block record length: [dQ_hi kF | dQ_lo kF | dcount k | changed |
+// recomputed | inertia_hi | inertia_lo] (lloyd.hip)
+__host__ __device__ inline int lloyd_rec(int k, int F) { return 2 * k * F + k + 4; }
+
+// x as an exact fixed-point integer: rint(x * 2^e) (|x * 2^e| < 2^41; fp64
+// holds it exactly, and sums of up to 2^12 of them).  Computed in fp32, then
+// widened: x * 2^e is exact in fp32 while it is a normal number (a power-of-two
+// scale of x, and |x * 2^e| < 2^41 cannot overflow); at or above 2^23 it is
+// already an integer, below it rintf's result is an integer < 2^23, so both
+// are exact; below 2^-126 both forms round to zero.  Same value as
+// rint(ldexp((double)x, e)), with one fp64 instruction instead of three.
+__device__ __forceinline__ double fixq64(float x, int e) {
+  float q = rintf(ldexpf(x, e));
+  asm("" : "+v"(q));  // keeps the fp32 ops (hipcc otherwise widens them back to fp64)
+  return (double)q;
+}
+__device__ __forceinline__ long long fixq(float x, int e) { return (long long)fixq64(x, e); }
+
+// int64 -> (hi, lo) integer-valued fp64 limbs
+__device__ __forceinline__ void limbs(long long v, double& hi, double& lo) {
+  const long long h = v >> 32;  // arithmetic shift: floor
+  hi = (double)h;
+  lo = (double)(v - h * (1LL << 32));
+}
+
 // ---- wave tiles: 64 consecutive rows of F floats (64*F floats, float4-aligned
 // because tile starts are multiples of 64 rows).  Each lane fetches NV =
 // FMAX/4 float4 with clamped, unconditional loads (guide §5.4c) and stores all

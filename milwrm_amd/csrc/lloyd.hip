@@ -61,33 +61,11 @@ struct LloydFitsArg {
   mw_lloyd_fit f[kMaxFits];
 };
 
-__host__ __device__ inline int lloyd_rec(int k, int F) { return 2 * k * F + k + 4; }
 __host__ __device__ inline size_t lloyd_al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // kList workspace after the G block records: per-block list lengths [G]
 // int32, then per-block lists of undecided row indices [G][R] int32
 __host__ __device__ inline size_t lloyd_list_off(int G, int k, int F) {
   return lloyd_al256((size_t)G * lloyd_rec(k, F) * sizeof(double));
-}
-
-// x as an exact fixed-point integer: rint(x * 2^e) (|x * 2^e| < 2^41; fp64
-// holds it exactly, and sums of up to 2^12 of them).  Computed in fp32, then
-// widened: x * 2^e is exact in fp32 while it is a normal number (a power-of-two
-// scale of x, and |x * 2^e| < 2^41 cannot overflow); at or above 2^23 it is
-// already an integer, below it rintf's result is an integer < 2^23, so both
-// are exact; below 2^-126 both forms round to zero.  Same value as
-// rint(ldexp((double)x, e)), with one fp64 instruction instead of three.
-__device__ __forceinline__ double fixq64(float x, int e) {
-  float q = rintf(ldexpf(x, e));
-  asm("" : "+v"(q));  // keeps the fp32 ops (hipcc otherwise widens them back to fp64)
-  return (double)q;
-}
-__device__ __forceinline__ long long fixq(float x, int e) { return (long long)fixq64(x, e); }
-
-// int64 -> (hi, lo) integer-valued fp64 limbs
-__device__ __forceinline__ void limbs(long long v, double& hi, double& lo) {
-  const long long h = v >> 32;  // arithmetic shift: floor
-  hi = (double)h;
-  lo = (double)(v - h * (1LL << 32));
 }
 
 // squared distance of the scaled row to one center (the same fp32 chain as
@@ -145,6 +123,7 @@ constexpr int kQueue = 2;  // stream only the row state; read the undecided rows
 constexpr int kFirstAtomic = 3;  // kFirst with the sums by LDS atomics (A/B)
 constexpr int kList = 4;  // kQueue as two launches: lloyd_mark_kernel lists, this kernel reads
 constexpr int kFirstSum = 7;  // kFirst with per-feature fp64 sums of label-sorted rows (internal, k <= 16)
+constexpr int kListGiven = 8;  // kList over lists already written (mw_lloyd_list_moved)
 
 // One pass of fit g = blockIdx.x % n over row block blockIdx.x / n (the n
 // blocks that read one row block are dispatched together: rows that several
@@ -844,6 +823,46 @@ __global__ void __launch_bounds__(256) lloyd_mark_kernel(const LloydFitsArg fits
   if (t == 0) reinterpret_cast<int*>(wsb + loff)[blk] = s_n;
 }
 
+// The kList row lists of a fold (mw_kpp_step_fold): per row block of the
+// Lloyd grid, the rows that move to the new center (bit *best of moved[]),
+// in the layout lloyd_mark_kernel writes; the list pass (kind 8) then
+// recomputes exactly those rows against the k final centers.
+__global__ void __launch_bounds__(256) lloyd_list_moved_kernel(const uint8_t* __restrict__ moved,
+                                                               const int* __restrict__ best, int64_t S,
+                                                               int64_t R, char* __restrict__ wsb, size_t loff,
+                                                               int G) {
+  __shared__ int s_n;
+  const int t = threadIdx.x, lane = t & 63;
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  const int b = *best;
+  const int blk = blockIdx.x;
+  int* __restrict__ list = reinterpret_cast<int*>(wsb + loff + lloyd_al256((size_t)G * 4)) + (size_t)blk * R;
+  const int64_t lo = (int64_t)blk * R, hi = min(S, lo + R);
+  for (int64_t r0 = lo + 4 * (int64_t)t; r0 < hi; r0 += 4 * 256) {  // lo is a multiple of 256
+    uint32_t m4 = 0;
+    if (r0 + 3 < hi) {
+      m4 = *reinterpret_cast<const uint32_t*>(moved + r0);
+    } else {
+      for (int i = 0; i < 4; ++i)
+        if (r0 + i < hi) m4 |= (uint32_t)moved[r0 + i] << (8 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool need = r0 + i < hi && ((m4 >> (8 * i + b)) & 1u);
+      const unsigned long long m = __ballot(need);
+      if (m != 0ull) {
+        int qb = 0;
+        if (lane == 0) qb = atomicAdd(&s_n, __popcll(m));
+        qb = __shfl(qb, 0, 64);
+        if (need) list[qb + __popcll(m & ((1ull << lane) - 1ull))] = (int)(r0 + i);
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) reinterpret_cast<int*>(wsb + loff)[blk] = s_n;
+}
+
 // one fit per blockIdx.y: fixed-order fold of its G block records
 __global__ void __launch_bounds__(256) lloyd_reduce_fits_kernel(const LloydFitsArg fits, int G, int F) {
   const mw_lloyd_fit& fit = fits.f[blockIdx.y];
@@ -939,6 +958,17 @@ int mw_col_absmax_acc(const float* d_X, int64_t S, int F, float* d_out, void* st
   return MW_OK;
 }
 
+int mw_lloyd_list_moved(const uint8_t* d_moved, const int* d_best, int64_t S, int F, int k, void* d_ws,
+                        void* stream) {
+  MW_CHECK_ARG(d_moved && d_best && d_ws && S > 0 && S < ((int64_t)1 << 31) && F > 0 && k >= 1,
+               "mw_lloyd_list_moved: bad arguments");
+  const int G = lloyd_blocks(S, F);
+  hipLaunchKernelGGL(lloyd_list_moved_kernel, dim3(G), dim3(256), 0, as_stream(stream), d_moved, d_best, S,
+                     lloyd_rows(S, F), static_cast<char*>(d_ws), lloyd_list_off(G, k, F), G);
+  MW_LAUNCH_CHECK();
+  return MW_OK;
+}
+
 int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const float* d_b,
                   const int32_t* d_qexp, int n, const mw_lloyd_fit* h_fits, int mode, int kind,
                   void* stream) {
@@ -946,7 +976,13 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   MW_CHECK_ARG(S > 0 && F > 0 && n >= 1 && n <= kMaxFits, "mw_lloyd_pass: bad shape (1 <= n <= %d)",
                kMaxFits);
   MW_CHECK_ARG(mode >= 0 && mode <= 2, "mw_lloyd_pass: bad mode %d", mode);
-  MW_CHECK_ARG(kind >= 0 && kind <= 6, "mw_lloyd_pass: bad kind %d", kind);
+  MW_CHECK_ARG(kind >= 0 && kind <= 6 || kind == kListGiven, "mw_lloyd_pass: bad kind %d", kind);
+  // kind 8: a kList pass over lists written beforehand (mw_lloyd_list_moved)
+  const bool lists_given = kind == kListGiven;
+  if (lists_given) {
+    MW_CHECK_ARG(mode == 0 && S < ((int64_t)1 << 31), "mw_lloyd_pass: kind 8 needs mode 0 and S < 2^31");
+    kind = kList;
+  }
   if (mode != 0) kind = kFirst;  // modes 1 and 2 stream every tile
   if (kind == kList && S >= ((int64_t)1 << 31)) kind = kQueue;  // int32 row lists
   LloydFitsArg fits{};
@@ -1048,7 +1084,7 @@ int mw_lloyd_pass(const float* d_X, int64_t S, int F, const float* d_a, const fl
   // FM = 52: the one-hot MFMA M-step takes 16-feature blocks (52 is not a multiple)
   if (mode == 0 && kind == kFirst && FM == 52) kind = kmax <= 16 ? kFirstSum : kFirstAtomic;
   const size_t lds = lloyd_lds_bytes(FM, kmax, F, mode, kind);
-  if (mode == 0 && kind == kList) {
+  if (mode == 0 && kind == kList && !lists_given) {
     hipLaunchKernelGGL(lloyd_mark_kernel, grid, dim3(256), 0, s, fits, n, S, F, R);
     MW_LAUNCH_CHECK();
   }

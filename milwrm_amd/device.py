@@ -170,11 +170,29 @@ def h2d_into(dst: torch.Tensor, a) -> None:
     _mark(slot)
 
 
-def d2h(*ts: torch.Tensor):
-    """Device tensors → host numpy arrays (fresh copies) with ONE stream
-    synchronisation: each is copied non-blocking into a pooled pinned buffer
-    (DMA straight into page-locked memory, no pageable staging by the
-    runtime).  Returns one array or a tuple."""
+class PendingD2H:
+    """Device → host copies queued by ``d2h_async``; ``wait()`` returns the
+    arrays (one or a tuple) after the copies, not after work queued later."""
+
+    def __init__(self, staged, ev):
+        self._staged, self._ev, self._out = staged, ev, None
+
+    def wait(self):
+        if self._out is None:
+            self._ev.synchronize()
+            arrs = tuple(v.numpy().copy().reshape(shape) for _, v, shape in self._staged)
+            for slot, _, _ in self._staged:
+                slot[1] = None
+            self._staged = ()
+            self._out = arrs[0] if len(arrs) == 1 else arrs
+        return self._out
+
+
+def d2h_async(*ts: torch.Tensor) -> PendingD2H:
+    """Queue device tensors → host copies: each is copied non-blocking into a
+    pooled pinned buffer (DMA straight into page-locked memory, no pageable
+    staging by the runtime), followed by an event.  The host may queue more
+    device work before it waits (``PendingD2H.wait``)."""
     staged = []
     for t in ts:
         t = t.contiguous()
@@ -184,11 +202,15 @@ def d2h(*ts: torch.Tensor):
         v = slot[0][:nbytes].view(t.dtype)
         v.copy_(t.reshape(-1), non_blocking=True)
         staged.append((slot, v, tuple(t.shape)))
-    torch.cuda.current_stream().synchronize()
-    arrs = tuple(v.numpy().copy().reshape(shape) for _, v, shape in staged)
-    for slot, _, _ in staged:
-        slot[1] = None
-    return arrs[0] if len(arrs) == 1 else arrs
+    ev = torch.cuda.Event()
+    ev.record()
+    return PendingD2H(staged, ev)
+
+
+def d2h(*ts: torch.Tensor):
+    """Device tensors → host numpy arrays (fresh copies) with ONE
+    synchronisation (on the copies).  Returns one array or a tuple."""
+    return d2h_async(*ts).wait()
 
 
 def dtype_code(t: torch.Tensor) -> int:

@@ -131,3 +131,31 @@ def test_c_fit_given_init_and_errors(gpu, golden):
         _c_fit(rows.X[:10], np.zeros(F), np.ones(F), 20)
     with pytest.raises(ValueError, match="max_iter"):
         _c_fit(rows.X, np.zeros(F), np.ones(F), 4, max_iter=0)
+
+
+@pytest.mark.parametrize("k,F", [(3, 30), (8, 30), (12, 17), (16, 32), (8, 8)])
+def test_kpp_fold_equals_separate_first_pass(gpu, monkeypatch, k, F):
+    """MW_KPP_FOLD=1 (the first Lloyd E-step folded into the last k-means++
+    pass, then the winner's moved rows through a kind-8 list pass) against
+    the separate kind-0 first pass: k-means++ indices, labels, centers,
+    inertia and n_iter bitwise, on overlapping clusters (many moved rows,
+    near ties)."""
+    import torch
+
+    from milwrm_amd import _native as N
+
+    assert N.load().mw_kpp_fold_supported(k, F, 2 + int(np.log(k))) == 1
+    rng = np.random.default_rng(100 + k)
+    S = 150_000 + 37 * k
+    cen = rng.normal(0, 1.5, size=(k + 3, F))
+    X = (cen[rng.integers(0, k + 3, S)] + rng.normal(0, 1.0, size=(S, F))).astype(np.float32)
+    X[:50] = X[50:100]  # exact duplicate rows: exact distance ties
+    Xd = torch.from_numpy(X).cuda()
+    mu, inv = X.mean(0).astype(np.float64), 1.0 / (X.std(0).astype(np.float64) + 0.5)
+    var = (np.var(X.astype(np.float64), axis=0) * inv * inv)
+    monkeypatch.setenv("MW_KPP_FOLD", "0")
+    a = _c_fit(Xd, mu, inv, k, var=var)
+    monkeypatch.setenv("MW_KPP_FOLD", "1")
+    b = _c_fit(Xd, mu, inv, k, var=var)
+    _same(a, b)
+    np.testing.assert_array_equal(a["idx"], b["idx"])

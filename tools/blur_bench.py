@@ -18,7 +18,7 @@ inv = ((torch.arange(C, device="cuda", dtype=torch.float32) * 37) % 11 + 1) * 1e
 ref = None
 variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["", "MW_BLUR_BH=256"]
 for bw in variants:
-    for kv in ("MW_BLUR_BH", "MW_BLUR_XCD", "MW_BLUR_BT"):
+    for kv in ("MW_BLUR_BH", "MW_BLUR_XCD", "MW_BLUR_BT", "MW_BLUR_BT8"):
         os.environ.pop(kv, None)
     for kv in filter(None, bw.split(";")):
         k, v = kv.split("=")
