@@ -383,6 +383,23 @@ def dense_pass_roofline(rows, ks=tuple(range(9, 21)), reps=6):
             "hbm_GBps": nbytes / t / 1e9, "frac_hbm": nbytes / t / 1e9 / HBM_PEAK_GBPS}
 
 
+def fit_rows_read(S, F, k):
+    """Rows whose features the last single fit of this thread read: k
+    k-means++ passes over all S rows plus, per Lloyd pass, the rows the pass
+    read (mw_kmeans_fit_history); None when the fit did not run in the C
+    driver (no history)."""
+    import numpy as np
+
+    from milwrm_amd import _native as N
+
+    n = N.load().mw_kmeans_fit_history(None, 0)
+    if n <= 0:
+        return None
+    h = np.zeros((n, 4), dtype=np.int64)
+    N.load().mw_kmeans_fit_history(h.ctypes.data, n)
+    return int(k * S + h[:, 3].sum())
+
+
 def host_outputs(lab):
     """Cost of the reference-format outputs of one slide, outside the timed
     step: ``tissue_IDs[0]`` and ``confidence_IDs[0]`` as float64 H x W host
@@ -591,6 +608,22 @@ def main():
         out["config"]["lloyd_iters"] = n_iter
         out["pipeline_roofline"] = {"algorithmic_bytes_per_slide": B, "achieved": pipe_gbps,
                                     "unit": "GB/s", "frac": pipe_gbps / (HBM_PEAK_GBPS * world)}
+        # the formula counts (k + n_iter + 1) full passes over the rows; the
+        # pruned Lloyd passes read only the rows their bounds leave open: the
+        # rows each pass of the last fit really read (mw_kmeans_fit_history)
+        fr = fit_rows_read(S, F, k)
+        if fr is not None:
+            formula_fit = (k + n_iter + 1) * S1 * F * 4
+            read_fit = fr / n_sl * F * 4
+            B_read = B - formula_fit + read_fit
+            out["pipeline_roofline"].update({
+                "fit_bytes_per_slide_formula": formula_fit, "fit_bytes_per_slide_read": read_fit,
+                "bytes_read_per_slide": B_read,
+                "achieved_bytes_read": B_read * world * n_sl / (elapsed / args.steps) / 1e9,
+                "note": "fit_bytes_per_slide_read: k k-means++ passes over every row + the rows each "
+                        "Lloyd pass of the rank's last fit read (its bounds skip the rest), x F x 4 B"})
+            out["pipeline_roofline"]["frac_bytes_read"] = (out["pipeline_roofline"]["achieved_bytes_read"]
+                                                           / (HBM_PEAK_GBPS * world))
     if not args.sweep and not args.no_host_outputs:
         out["host_outputs"] = host_outputs(lab)
     if (world == 1 and not args.sweep and args.mode == "hard" and not args.no_design_point

@@ -295,6 +295,9 @@ int mw_kpp_trial(const float* d_X, int64_t S, int F, const double* d_mu,
  *             (mw_lloyd_ws_bytes_kinds(S, k, F, 0): records only, no kind 4)
  *   out       mw_lloyd_rec_len(k, F) fp64, the fixed-order fold of the records:
  *             [dQ_hi k*F | dQ_lo k*F | dcount k | changed | recomputed | in_hi | in_lo]
+ *             (mode 0: in_hi * 2^32 + in_lo = the rows whose features the pass
+ *             read -- all of them for kinds 0 / 1, the queued or listed ones
+ *             for kinds 2 / 4; 0 for the dense kinds)
  * mode 0: E-step (rows whose bounds prove the label skip the distances) and
  *         the M-step change of the per-cluster sums: every raw value rounds
  *         once to q = rint(x * 2^qexp[f]) (|q| < 2^41) and a relabelled row
@@ -343,6 +346,13 @@ int mw_col_absmax(const float* d_X, int64_t S, int F, float* d_out, void* stream
 /* The same maxima folded into d_out (fp32 [F], >= 0) without resetting it:
  * the column maxima of a slide processed band after band. */
 int mw_col_absmax_acc(const float* d_X, int64_t S, int F, float* d_out, void* stream);
+
+/* Per pass of the calling thread's last mw_kmeans_fit / mw_kmeans_fit_async
+ * (k-means++ passes excluded): 4 int64 each -- kind (0..8; 10 + mode for the
+ * final pass), rows relabelled, rows recomputed, rows whose features the pass
+ * read -- up to cap passes into out; returns the number of passes.  For the
+ * measurement of the bytes a pruned fit really reads (bench.py). */
+int mw_kmeans_fit_history(int64_t* out, int cap);
 
 /* ---- whole fit: sklearn KMeans(algorithm="lloyd").fit (_kmeans.py:1427-1554)
  * Replaces the reference's `KMeans(n_clusters=k, random_state=seed).fit(X)`

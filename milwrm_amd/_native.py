@@ -62,6 +62,7 @@ _PROTOS = {
                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mw_kpp_fold_rec_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "mw_kpp_fold_supported": (c_i32, [c_i32, c_i32, c_i32]),
+    "mw_kmeans_fit_history": (c_i32, [c_vp, c_i32]),
     "mw_kpp_best_ptr": (c_vp, [c_vp, c_i64, c_i32]),
     "mw_kpp_pots": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mw_kpp_search": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),

@@ -411,6 +411,16 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
                            double* h_inertia, int* h_n_iter, int64_t* h_init_idx, void* d_ws, size_t ws_bytes,
                            double* h_final_rec, int* h_inertia_exp, void* stream);
 
+// per pass of the thread's last single fit: kind, changed, recomputed, rows read
+static thread_local std::vector<int64_t> fit_hist;
+
+extern "C" int mw_kmeans_fit_history(int64_t* out, int cap) {
+  const int n = (int)(fit_hist.size() / 4);
+  if (out)
+    for (int i = 0; i < std::min(n, cap) * 4; ++i) out[i] = fit_hist[i];
+  return n;
+}
+
 extern "C" int mw_kmeans_fit(const float* d_X, int64_t S, int F, const double* h_mu,
                              const double* h_inv, const double* h_feature_var, const float* h_xmax,
                              int k, const double* h_init, uint32_t seed, int max_iter, double tol,
@@ -602,6 +612,7 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
   }
 
   // Lloyd iterations (the fold pass labelled every row already)
+  fit_hist.clear();
   if (!fold) MW_HIP(hipMemsetAsync(d_labels, 255, (size_t)S, st));
   std::vector<int64_t> q_hi((size_t)k * F, 0), q_lo((size_t)k * F, 0), count(k, 0);
   std::vector<double> rec, cnew((size_t)k * F), weight(k), tmp(std::max(F, k));
@@ -645,6 +656,8 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
     const double* tail = rec.data() + 2 * (size_t)k * F + k;
     const int64_t changed = (int64_t)tail[0];
     last_recomputed = (int64_t)tail[1];
+    fit_hist.insert(fit_hist.end(), {(int64_t)(fold && it == 0 ? 8 : kind), changed, last_recomputed,
+                                     (int64_t)(tail[2] * 4294967296.0 + tail[3])});
     for (int j = 0; j < k; ++j) {
       weight[j] = (double)count[j];
       for (int f = 0; f < F; ++f) {
@@ -734,6 +747,7 @@ static int kmeans_fit_impl(const float* d_X, int64_t S, int F, const double* h_m
   const double xc = xnorm + cmax;
   const int iexp = exp_below(xc * xc * 1.01);
   MW_TRY(fit.upload(centers));
+  fit_hist.insert(fit_hist.end(), {(int64_t)(strict ? 12 : 11), -1, -1, S});  // the final pass reads every row
   *h_n_iter = n_iter;
   std::memcpy(h_centers, centers.data(), centers.size() * sizeof(double));
   if (h_final_rec && !own.p && pinned_staging()) {  // (a workspace allocated here is freed on return: synchronous end)

@@ -639,12 +639,12 @@ __global__ void __launch_bounds__(512, 4) kpp_fold_kernel(
     out[kf * F + q] = l;
   }
   for (int j = t; j < kf; j += blockDim.x) out[2 * kf * F + j] = (double)s_cnt[j];
-  if (t == 0) {  // every row changed from unlabelled and was computed
+  if (t == 0) {  // every row changed from unlabelled, was computed and read
     const double nv = (double)(hi > lo ? hi - lo : 0);
     out[2 * kf * F + kf] = nv;
     out[2 * kf * F + kf + 1] = nv;
     out[2 * kf * F + kf + 2] = 0.0;
-    out[2 * kf * F + kf + 3] = 0.0;
+    out[2 * kf * F + kf + 3] = nv;
   }
 }
 

@@ -379,6 +379,7 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
       }
       __syncthreads();
       const int nq = s_qn;
+      if (t == 0) inert += nq;  // mode 0: the record's inertia slots count the rows read
       // ---- phase 2: the queued rows, 64 per wave batch ----
       for (int e0 = wid * 64; e0 < nq; e0 += nw * 64) {
         const int cnt_b = min(64, nq - e0);
@@ -447,6 +448,7 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
     const char* wsb = reinterpret_cast<const char*>(fit.ws);
     const size_t loff = lloyd_list_off(G, k, F);
     const int nq = reinterpret_cast<const int*>(wsb + loff)[blk];
+    if (t == 0) inert = nq;  // mode 0: the record's inertia slots count the rows read
     const int* __restrict__ list =
         reinterpret_cast<const int*>(wsb + loff + lloyd_al256((size_t)G * 4)) + (size_t)blk * R;
     int* s_row = s_lab;  // the batch's 64 row indices (per wave)
@@ -476,6 +478,7 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
     }
   } else {
     // ========================== streamed tiles ==========================
+    if (MODE == 0 && t == 0) inert = nb;  // mode 0: the record's inertia slots count the rows read
     const int ntile = hi > lo ? (int)((hi - lo + 63) / 64) : 0;
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(X + lo * F, (S - lo) * F * 4);
     const __amdgpu_buffer_rsrc_t rl = make_rsrc(labels + lo, nb);
