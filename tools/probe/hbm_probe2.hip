@@ -1,0 +1,107 @@
+// HBM read-ceiling probe at the step's own stream sizes: how fast can a
+// plain streaming read-reduce go over 2.2 GB (one k-means++ / Lloyd pass at
+// config 2) and over 6 GB, with zero-filled vs random data, and with the
+// default vs non-temporal load policy.  Grid = CUs x blocks-per-CU, 256-thread
+// blocks, U 16-byte loads in flight per lane (grid-stride).
+// usage: hbm_probe2 <GB> <fill: 0 zeros | 1 random>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) rd(const f4* __restrict__ x, long n4, float* out) {
+  const long stride = (long)gridDim.x * 256 * U;
+  f4 acc = {0, 0, 0, 0};
+  for (long i = (long)blockIdx.x * 256 * U + threadIdx.x; i < n4; i += stride) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      long j = i + u * 256;
+      j = j < n4 ? j : n4 - 1;
+      v[u] = NT ? __builtin_nontemporal_load(x + j) : x[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+  }
+  if (acc.x + acc.y + acc.z + acc.w == 1234.5f) out[0] = 1.f;
+}
+
+// the same bytes in contiguous per-block chunks (each block one slice of the
+// buffer, as the row-streaming kernels' static partitions do)
+template <int U>
+__global__ void __launch_bounds__(256) rd_chunk(const f4* __restrict__ x, long n4, float* out) {
+  const long per = (n4 + gridDim.x - 1) / gridDim.x;
+  const long lo = (long)blockIdx.x * per, hi = lo + per < n4 ? lo + per : n4;
+  f4 acc = {0, 0, 0, 0};
+  for (long i = lo + threadIdx.x; i < hi; i += 256 * U) {
+    f4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      long j = i + u * 256;
+      v[u] = x[j < hi ? j : hi - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+  }
+  if (acc.x + acc.y + acc.z + acc.w == 1234.5f) out[0] = 1.f;
+}
+
+__global__ void fill_random(unsigned* p, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    unsigned h = (unsigned)i * 2654435761u ^ (unsigned)(i >> 32) * 40503u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    p[i] = (h & 0x3fffffffu) | 0x3f000000u;  // finite positive floats
+  }
+}
+
+template <typename L>
+static float timeit(L launch, int reps) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  launch();
+  hipEventRecord(a);
+  for (int r = 0; r < reps; ++r) launch();
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return ms / reps;
+}
+
+int main(int argc, char** argv) {
+  const double gb = argc > 1 ? atof(argv[1]) : 2.2;
+  const int fill = argc > 2 ? atoi(argv[2]) : 1;
+  const long bytes = ((long)(gb * 1e9) / 4096) * 4096;
+  const long n4 = bytes / 16;
+  f4* x;
+  float* o;
+  if (hipMalloc(&x, bytes) || hipMalloc(&o, 64)) return 1;
+  if (fill)
+    hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned*)x, bytes / 4);
+  else
+    hipMemset(x, 0, bytes);
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  int ncu;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+  printf("CUs %d, stream %.2f GB, fill %s\n", ncu, bytes / 1e9, fill ? "random" : "zeros");
+  for (int bpc : {2, 4, 8}) {
+    const int g = ncu * bpc;
+#define RUN(U)                                                                                         \
+  {                                                                                                    \
+    float t1 = timeit([&] { hipLaunchKernelGGL((rd<U, false>), dim3(g), dim3(256), 0, 0, x, n4, o); }, 10); \
+    float t2 = timeit([&] { hipLaunchKernelGGL((rd<U, true>), dim3(g), dim3(256), 0, 0, x, n4, o); }, 10);  \
+    float t3 = timeit([&] { hipLaunchKernelGGL((rd_chunk<U>), dim3(g), dim3(256), 0, 0, x, n4, o); }, 10);  \
+    printf("blocks/CU %d U %d: read %.0f GB/s (%.1f us)  nt %.0f GB/s  chunked %.0f GB/s\n", bpc, U,  \
+           bytes / t1 / 1e6, t1 * 1e3, bytes / t2 / 1e6, bytes / t3 / 1e6);                           \
+  }
+    RUN(2) RUN(4) RUN(8)
+  }
+  return 0;
+}
