@@ -87,7 +87,10 @@ __device__ __forceinline__ void lds_barrier() {
 // drains it: the kernel waits for it with counted vmcnt before the barrier
 // that precedes the read.  The offset VGPR is set once per thread and never
 // rewritten, so no later instruction can race the DMA's operand read; the
-// string opens with s_nop 4 (SGPR base fresh from VALU/readfirstlane).
+// string opens with s_nop 4 (SGPR base fresh from VALU/readfirstlane).  The
+// default cache policy: with nt (the row passes' kStreamAux) the launch takes
+// 4.21 instead of 4.11 ms (the bands' column halos are L2 hits;
+// profiles/r06/nt_ab*/).
 __device__ __forceinline__ void glds16(const void* sbase, uint32_t voff, uint32_t lds_dst) {
   unsigned keep;
   asm volatile(

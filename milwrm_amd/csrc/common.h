@@ -31,6 +31,20 @@ void set_error(const char* fmt, ...);
     }                                                                       \
   } while (0)
 
+// read-once loads of the row streams with the streaming (nt) cache policy
+// (MW_STREAM_NT=0: the default policy, for same-box A/B builds).  Same-box
+// A/B at config 2 (profiles/r06/nt_ab*/): k-means++ step pass 495 -> 457 us,
+// Lloyd kind-1 pass 451 -> 399, label pass 2.74 -> 2.67 ms, gather -1 %; the
+// blur and the nonzero statistics kept the default policy (nt: +2.5 / +3 %)
+#ifndef MW_STREAM_NT
+#define MW_STREAM_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (MW_STREAM_NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 #define MW_LAUNCH_CHECK()                                                   \
   do {                                                                      \
     hipError_t e_ = hipGetLastError();                                      \

@@ -228,13 +228,13 @@ __global__ void __launch_bounds__(256, kAssignWPS) assign_kernel(const float* __
   auto fetch = [&](f4v (&vv)[NV], int& mm, int tt) {
     tt = tt < ntile ? tt : ntile - 1;
     const int64_t r = lo + (int64_t)tt * 64;
-    mm = mask[min(r + lane, hi - 1)];
+    mm = ld_stream(mask + min(r + lane, hi - 1));  // nt: read-once streams
     const int64_t q0 = (r * C) >> 2;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       int64_t q = q0 + lane + i * 64;
       q = q < n4 ? q : n4 - 1;
-      vv[i] = X4[q];
+      vv[i] = ld_stream(X4 + q);
     }
   };
   auto body = [&](f4v (&vv)[NV], int& mm, int tc) {

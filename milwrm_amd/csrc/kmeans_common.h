@@ -80,6 +80,13 @@ __device__ __forceinline__ void wt_tail(int nfl, int64_t e0, int64_t n4, const f
   }
 }
 
+// cache policy of the row streams' loads (buffer aux bits; 2 = nt,
+// streaming): every pass reads its rows once and a pass's rows (>= 2 GB at
+// config 2) do not fit the caches, so the loads need not allocate; a plain
+// 2.2-GB read goes 6.3 -> 7.1 TB/s (tools/probe/hbm_probe2.hip,
+// profiles/r06/hbm_probe2.txt; common.h MW_STREAM_NT for the passes' A/B)
+constexpr int kStreamAux = MW_STREAM_NT ? 2 : 0;
+
 // ---- wave-tile streaming with buffer loads: the resource covers a block's
 // rows from its first row to the end of the array (32-bit block-relative
 // offsets, hardware range check), the tile offset is a scalar (tile index is
@@ -95,7 +102,7 @@ template <int NV>
 __device__ __forceinline__ void tile_load(__amdgpu_buffer_rsrc_t rs, int soff, int lane, f4v (&v)[NV]) {
 #pragma unroll
   for (int i = 0; i < NV; ++i)
-    v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + i * 1024, soff, 0));
+    v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + i * 1024, soff, kStreamAux));
 }
 
 // ---- E-step center stream, written as inline asm so that the schedule is

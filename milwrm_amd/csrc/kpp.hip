@@ -276,11 +276,11 @@ __global__ void __launch_bounds__(256, FMAX == 64 ? 2 : 4) kpp_pass_kernel(
   auto fetch = [&](int tt) {
     tt = tt < ntile ? tt : ntile - 1;
     if (MODE != 0)
-      cur_next = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, lane * 8, tt * 512, 0));
+      cur_next = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, lane * 8, tt * 512, kStreamAux));
 #pragma unroll
     for (int i = 0; i < NV; ++i)  // only the vectors that hold the tile's 64 x F floats
       if (!FS || i * 1024 < tile_bytes)
-        v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16 + i * 1024, tt * tile_bytes, 0));
+        v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16 + i * 1024, tt * tile_bytes, kStreamAux));
   };
   int tc = wid;
   if (tc < ntile) fetch(tc);
@@ -504,10 +504,10 @@ __global__ void __launch_bounds__(512, 4) kpp_fold_kernel(
     double cur_next = 0.0;
     auto fetch = [&](int tt) {
       tt = tt < ntile ? tt : ntile - 1;
-      cur_next = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, lane * 8, tt * 512, 0));
+      cur_next = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, lane * 8, tt * 512, kStreamAux));
 #pragma unroll
       for (int i = 0; i < NV; ++i)
-        v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16 + i * 1024, tt * tile_bytes, 0));
+        v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16 + i * 1024, tt * tile_bytes, kStreamAux));
     };
     if (w4 < ntile) fetch(w4);
     for (int it = 0; it < nround; ++it) {

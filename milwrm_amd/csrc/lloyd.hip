@@ -537,14 +537,14 @@ __device__ __forceinline__ void lloyd_pass_body(const float* __restrict__ X, int
       tt = tt < ntile ? tt : ntile - 1;
       lab_next = __builtin_amdgcn_raw_buffer_load_b8(rl, lane, tt * 64, 0);
       if (BOUNDS) {
-        ub_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ru, lane * 4, tt * 256, 0));
-        lb_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, lane * 4, tt * 256, 0));
+        ub_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ru, lane * 4, tt * 256, kStreamAux));
+        lb_next = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rw, lane * 4, tt * 256, kStreamAux));
       }
 #pragma unroll
       for (int i = 0; i < NV; ++i)  // only the vectors that hold the tile's 64 x F floats
         if (FMAX != 64 || i * 1024 < tile_bytes)
           v[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, lane * 16 + i * 1024,
-                                                                               tt * tile_bytes, 0));
+                                                                               tt * tile_bytes, kStreamAux));
     };
     int tc = wid;
     if (tc < ntile) fetch(tc);

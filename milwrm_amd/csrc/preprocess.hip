@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const float* __restrict__ i
 #pragma unroll
       for (int i = 0; i < kBatch; ++i) {
         const int row = min(wid * 64 + (i0 + i) * RPI + lr, nrow - 1);  // clamped: always valid
-        v[i] = GATHER ? img[(int64_t)pix[row] * C + fcol] : X[(r0 + row) * F + fcol];
+        v[i] = GATHER ? ld_stream(img + (int64_t)pix[row] * C + fcol) : X[(r0 + row) * F + fcol];
       }
 #pragma unroll
       for (int i = 0; i < kBatch; ++i) {
