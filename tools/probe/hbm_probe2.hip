@@ -48,6 +48,49 @@ __global__ void __launch_bounds__(256) rd_chunk(const f4* __restrict__ x, long n
   if (acc.x + acc.y + acc.z + acc.w == 1234.5f) out[0] = 1.f;
 }
 
+// the row passes' access shape: 256-thread blocks, each wave streams 64-row x
+// 128-B tiles (8 KB, eight 16-B loads per lane), the next tile's loads issued
+// before the current one is consumed, COMP fp64 FMAs per lane per tile (the
+// k-means++ pass does ~300).  IL = 0: block b owns a contiguous tile range
+// (waves interleaved inside it, as kpp_pass_kernel); IL = 1: tiles interleaved
+// over every wave of the grid (as the label pass's il = 1).
+template <int IL, bool NT, int COMP>
+__global__ void __launch_bounds__(256) tile_rd(const f4* __restrict__ x, long ntiles, float* out) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = 4;
+  long t0, tstep, tend;
+  if (IL) {
+    t0 = (long)blockIdx.x * nw + wid; tstep = (long)gridDim.x * nw; tend = ntiles;
+  } else {
+    const long per = (ntiles + gridDim.x - 1) / gridDim.x;
+    const long lo = (long)blockIdx.x * per;
+    t0 = lo + wid; tstep = nw; tend = lo + per < ntiles ? lo + per : ntiles;
+  }
+  f4 v[8], acc = {0, 0, 0, 0};
+  double d0 = lane, d1 = 1.0 + lane, d2 = 2.0, d3 = 3.0;
+  auto fetch = [&](long t) {
+    t = t < tend ? t : tend - 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f4* p = x + t * 512 + lane + i * 64;
+      v[i] = NT ? __builtin_nontemporal_load(p) : *p;
+    }
+  };
+  if (t0 < tend) fetch(t0);
+  for (long t = t0; t < tend; t += tstep) {
+    f4 cur[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cur[i] = v[i];
+    fetch(t + tstep);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += cur[i];
+    const double xv = acc.x;
+    for (int c = 0; c < COMP / 4; ++c) {
+      d0 = fma(d0, xv, 1e-9); d1 = fma(d1, xv, 1e-9); d2 = fma(d2, xv, 1e-9); d3 = fma(d3, xv, 1e-9);
+    }
+  }
+  if (acc.x + acc.y + acc.z + acc.w + (float)(d0 + d1 + d2 + d3) == 1234.5f) out[0] = 1.f;
+}
+
 __global__ void fill_random(unsigned* p, long n) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     unsigned h = (unsigned)i * 2654435761u ^ (unsigned)(i >> 32) * 40503u;
@@ -103,5 +146,14 @@ int main(int argc, char** argv) {
   }
     RUN(2) RUN(4) RUN(8)
   }
+  const long ntiles = n4 / 512;
+  const int g4 = ncu * 4;
+#define TRUN(IL, NT, COMP)                                                                                  \
+  {                                                                                                         \
+    float t = timeit([&] { hipLaunchKernelGGL((tile_rd<IL, NT, COMP>), dim3(g4), dim3(256), 0, 0, x, ntiles, o); }, 10); \
+    printf("tiles il %d nt %d comp %3d: %.0f GB/s (%.1f us)\n", IL, (int)NT, COMP, ntiles * 8192.0 / t / 1e6, t * 1e3); \
+  }
+  TRUN(0, false, 0) TRUN(0, true, 0) TRUN(1, false, 0) TRUN(1, true, 0)
+  TRUN(0, false, 300) TRUN(0, true, 300) TRUN(1, false, 300) TRUN(1, true, 300)
   return 0;
 }
