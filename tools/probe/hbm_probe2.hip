@@ -91,6 +91,54 @@ __global__ void __launch_bounds__(256) tile_rd(const f4* __restrict__ x, long nt
   if (acc.x + acc.y + acc.z + acc.w + (float)(d0 + d1 + d2 + d3) == 1234.5f) out[0] = 1.f;
 }
 
+// the k-means++ pass's data movement without its arithmetic: MODE 1 = the
+// tile through LDS (each lane writes its eight 16-B pieces, then reads its own
+// row as 16 feature pairs, as kpp_pass_kernel); MODE 2 = no LDS, each lane
+// loads its own 128-B row directly (eight 16-B loads, 64 lines per
+// instruction); both nt, IL = 0 (block-contiguous tiles)
+template <int MODE>
+__global__ void __launch_bounds__(256) tile_rows(const f4* __restrict__ x, long ntiles, float* out) {
+  __shared__ __attribute__((aligned(16))) float s_tile[4][64 * 32];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = 4;
+  const long per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const long lo = (long)blockIdx.x * per;
+  const long t0 = lo + wid, tstep = nw, tend = lo + per < ntiles ? lo + per : ntiles;
+  f4 v[8];
+  double acc = 0.0;
+  auto fetch = [&](long t) {
+    t = t < tend ? t : tend - 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f4* p = MODE == 2 ? x + t * 512 + lane * 8 + i : x + t * 512 + lane + i * 64;
+      v[i] = __builtin_nontemporal_load(p);
+    }
+  };
+  if (t0 < tend) fetch(t0);
+  for (long t = t0; t < tend; t += tstep) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 row[16];
+    if (MODE == 1) {
+      f4* s4 = reinterpret_cast<f4*>(s_tile[wid]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s4[lane + i * 64] = v[i];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      fetch(t + tstep);
+      const f2* r2 = reinterpret_cast<const f2*>(s_tile[wid] + lane * 32);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) row[p] = r2[p];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { row[2 * i] = f2{v[i].x, v[i].y}; row[2 * i + 1] = f2{v[i].z, v[i].w}; }
+      fetch(t + tstep);
+    }
+#pragma unroll
+    for (int p = 0; p < 16; ++p) acc = fma((double)row[p].x, (double)row[p].y, acc);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (acc == 1234.5) out[0] = 1.f;
+}
+
 __global__ void fill_random(unsigned* p, long n) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     unsigned h = (unsigned)i * 2654435761u ^ (unsigned)(i >> 32) * 40503u;
@@ -155,5 +203,11 @@ int main(int argc, char** argv) {
   }
   TRUN(0, false, 0) TRUN(0, true, 0) TRUN(1, false, 0) TRUN(1, true, 0)
   TRUN(0, false, 300) TRUN(0, true, 300) TRUN(1, false, 300) TRUN(1, true, 300)
+  {
+    float t1 = timeit([&] { hipLaunchKernelGGL((tile_rows<1>), dim3(g4), dim3(256), 0, 0, x, ntiles, o); }, 10);
+    float t2 = timeit([&] { hipLaunchKernelGGL((tile_rows<2>), dim3(g4), dim3(256), 0, 0, x, ntiles, o); }, 10);
+    printf("rows via LDS: %.0f GB/s (%.1f us)  rows direct: %.0f GB/s (%.1f us)\n", ntiles * 8192.0 / t1 / 1e6,
+           t1 * 1e3, ntiles * 8192.0 / t2 / 1e6, t2 * 1e3);
+  }
   return 0;
 }
