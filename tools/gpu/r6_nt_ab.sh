@@ -4,6 +4,10 @@
 # alternating; then the step time of each; with FP=1 first the variant's fit
 # fingerprint.  "nt" = the default library, "nont" = the variant.
 #   r6_nt_ab.sh TAG [VARIANT_LIB]
+# The variant is built here first, e.g. MW_BUILD_DIR=build_nont
+# MW_LIB=milwrm_amd/lib_nont.so MW_EXTRA_FLAGS=-DMW_STREAM_NT=0 python -m
+# milwrm_amd.build, and must travel (.gpurunignore lists milwrm_amd/lib_*.so:
+# narrow that pattern while the A/B runs).
 set -o pipefail
 TAG=${1:-r6ntab}
 VLIB=${2:-lib_nont.so}
