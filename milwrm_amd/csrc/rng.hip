@@ -123,39 +123,73 @@ __global__ void __launch_bounds__(kRngThreads) mt_jump_kernel(uint32_t* __restri
   if (i < kN) dst[i] = acc[i];
 }
 
-// per segment: regenerate L words, temper, masked rejection, ordered compaction
-__global__ void __launch_bounds__(kRngThreads) mt_gen_kernel(const uint32_t* __restrict__ states,
-                                                             int64_t L, uint32_t mask, uint32_t rng,
-                                                             uint32_t* __restrict__ tmp,
-                                                             int64_t* __restrict__ cnt) {
+// in-place regeneration of a 624-word LDS window by one wave (no workgroup
+// barriers): each phase reads all its old words, then writes; a wave's LDS
+// operations complete in order, and the wavefront fence keeps the compiler
+// from moving a lane's store above another lane's load of the same word
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+template <int LO, int HI, int OFF2>
+__device__ __forceinline__ void regen_phase(uint32_t* a, int lane) {
+  constexpr int R = (HI - LO + 63) / 64;
+  uint32_t v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = LO + r * 64 + lane;
+    if (i < HI) v[r] = twist(a[i], a[i + 1 < kN ? i + 1 : 0], a[i + OFF2]);
+  }
+  wave_fence();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = LO + r * 64 + lane;
+    if (i < HI) a[i] = v[r];
+  }
+  wave_fence();
+}
+__device__ __forceinline__ void regen_wave(uint32_t* a, int lane) {
+  regen_phase<0, 227, kM>(a, lane);
+  regen_phase<227, 454, kM - kN>(a, lane);
+  regen_phase<454, kN, kM - kN>(a, lane);
+}
+
+// per segment (one wave each): regenerate L words, temper, masked rejection,
+// ordered compaction (word 64 r + lane: ballot per r, in word order).  One
+// wave per segment: the former 10-wave workgroup spent 8 workgroup barriers
+// per 624 words (mt_gen 0.61 ms per config-2 draw -> 0.35 ms, mt_scatter 0.22
+// -> 0.18 ms with the 624 x 32-word segments).  Staging the compacted words in
+// an LDS ring for aligned 256-B stores measured slower (0.50 ms), and the
+// segment length does not matter between 624 x 8 and x 32 (0.34 / 0.35 ms)
+__global__ void __launch_bounds__(64) mt_gen_kernel(const uint32_t* __restrict__ states,
+                                                    int64_t L, uint32_t mask, uint32_t rng,
+                                                    uint32_t* __restrict__ tmp,
+                                                    int64_t* __restrict__ cnt) {
   __shared__ uint32_t a[kN];
-  __shared__ int s_w[kRngThreads / 64];
-  const int w = blockIdx.x, i = threadIdx.x, lane = i & 63, wid = i >> 6;
-  if (i < kN) a[i] = states[(size_t)w * kN + i];
-  __syncthreads();
+  const int w = blockIdx.x, lane = threadIdx.x;
+  for (int i = lane; i < kN; i += 64) a[i] = states[(size_t)w * kN + i];
+  wave_fence();
   uint32_t* out = tmp + (size_t)w * L;
   int64_t count = 0;
-  for (int64_t blk = 0; blk < L / kN; ++blk) {
-    regen_lds(a);
-    uint32_t v = 0;
-    bool ok = false;
-    if (i < kN) {
-      v = temper(a[i]) & mask;
-      ok = v <= rng;
+  const int64_t nblk = L / kN;
+  for (int64_t blk = 0; blk < nblk; ++blk) {
+    regen_wave(a, lane);
+#pragma unroll
+    for (int r = 0; r < (kN + 63) / 64; ++r) {
+      const int i = r * 64 + lane;
+      uint32_t v = 0;
+      bool ok = false;
+      if (i < kN) {
+        v = temper(a[i]) & mask;
+        ok = v <= rng;
+      }
+      const unsigned long long m = __ballot(ok);
+      if (ok) out[count + __popcll(m & ((1ull << lane) - 1ull))] = v;
+      count += __popcll(m);
     }
-    const unsigned long long m = __ballot(ok);
-    if (lane == 0) s_w[wid] = __popcll(m);
-    __syncthreads();
-    int base = 0, tot = 0;
-    for (int q = 0; q < kRngThreads / 64; ++q) {
-      if (q < wid) base += s_w[q];
-      tot += s_w[q];
-    }
-    if (ok) out[count + base + __popcll(m & ((1ull << lane) - 1ull))] = v;
-    count += tot;
-    __syncthreads();
+    wave_fence();  // the next regeneration's stores after this pass's loads
   }
-  if (i == 0) cnt[w] = count;
+  if (lane == 0) cnt[w] = count;
 }
 
 __global__ void __launch_bounds__(1024) mt_scan_kernel(int64_t* __restrict__ cnt, int W,
@@ -266,13 +300,13 @@ int mw_mt_segment_states(uint32_t seed, int64_t W, const uint64_t* d_tables, int
 static int randint_gen(const uint32_t* states, const RngPlan& p, int64_t size, int64_t L,
                        int32_t* d_out, int64_t* d_total, uint32_t* tmp, int64_t* cnt,
                        hipStream_t st) {
-  hipLaunchKernelGGL(mt_gen_kernel, dim3((unsigned)p.W), dim3(kRngThreads), 0, st, states, L, p.mask,
+  hipLaunchKernelGGL(mt_gen_kernel, dim3((unsigned)p.W), dim3(64), 0, st, states, L, p.mask,
                      p.rng, tmp, cnt);
   MW_LAUNCH_CHECK();
   MW_CHECK_ARG(p.W <= 1024 * 1024, "mw_legacy_randint: too many segments");
   hipLaunchKernelGGL(mt_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, (int)p.W, d_total);
   MW_LAUNCH_CHECK();
-  const unsigned gx = (unsigned)std::min<int64_t>((L + 255) / 256, 64);
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((L + 8191) / 8192, 64));
   hipLaunchKernelGGL(mt_scatter_kernel, dim3(gx, (unsigned)p.W), dim3(256), 0, st, tmp, cnt,
                      d_total, (int)p.W, L, size, d_out);
   MW_LAUNCH_CHECK();

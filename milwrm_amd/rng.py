@@ -36,7 +36,13 @@ def subsample_indices(M: int, fract: float, random_state: int = 16, out=None) ->
 
 
 # ---- device generator (MT19937 jump-ahead, csrc/rng.hip) -------------------
-MT_SEGMENT = 624 * 128   # words per segment
+# words per segment: 32 regenerations of the 624-word window.  mt_gen runs one
+# wave per segment through its regenerations in order, so the segment length
+# is its serial chain: ~1,150 segments for the config-2 draw (~23 M words),
+# 4-5 waves per CU.  The start states (one 2.5-KB window per segment, built
+# once per process by the jump prefix): 5 MB at config 2, 82 MB for a
+# 40k^2-pixel slide's draw.
+MT_SEGMENT = 624 * 32
 MT_LEVELS = 24           # jump tables t^(L 2^j) mod phi, j < 24 (2^24 segments)
 _tables = {}
 
@@ -114,7 +120,7 @@ def set_global_state_after_draws() -> None:
     accepted counts (exclusive offsets after its scan) the segment holding the
     S-th accepted draw is known; its start state is the MT19937 recurrence
     window after w*L words, i.e. NumPy's key with pos = 624; the host replays
-    at most one segment (L = 79,872 words, ~1 ms) to find the word that
+    at most one segment (L = 19,968 words) to find the word that
     accepted draw S came from.  Call after the draw has been synchronised."""
     import torch
 
