@@ -97,8 +97,12 @@ __global__ void __launch_bounds__(256) tile_rd(const f4* __restrict__ x, long nt
 // loads its own 128-B row directly (eight 16-B loads, 64 lines per
 // instruction); both nt, IL = 0 (block-contiguous tiles)
 template <int MODE>
-__global__ void __launch_bounds__(256) tile_rows(const f4* __restrict__ x, long ntiles, float* out) {
+__global__ void __launch_bounds__(256) tile_rows(const f4* __restrict__ x, long ntiles, float* out,
+                                                 double* __restrict__ cur = nullptr,
+                                                 double* __restrict__ tsum = nullptr) {
   __shared__ __attribute__((aligned(16))) float s_tile[4][64 * 32];
+  __shared__ double s_cur[4][8][64];  // MODE 8 / 9: cur updates of the wave's last NB tiles
+  constexpr int NB = MODE == 9 ? 8 : 4;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = 4;
   const long per = (ntiles + gridDim.x - 1) / gridDim.x;
   const long lo = (long)blockIdx.x * per;
@@ -117,7 +121,12 @@ __global__ void __launch_bounds__(256) tile_rows(const f4* __restrict__ x, long 
   for (long t = t0; t < tend; t += tstep) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     f2 row[16];
-    if (MODE == 1) {
+    // MODE 3 / 4: the k-means++ pass's side streams: the row's cur (8 B per
+    // lane, nt load) and its update (8-B store per lane); MODE 3 also one 8-B
+    // tile sum per tile (lane 0, tsum[t])
+    double cd = 0.0;
+    if (MODE >= 3 && MODE != 6) cd = __builtin_nontemporal_load(cur + t * 64 + lane);
+    if (MODE >= 1 && MODE != 2) {
       f4* s4 = reinterpret_cast<f4*>(s_tile[wid]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s4[lane + i * 64] = v[i];
@@ -134,6 +143,21 @@ __global__ void __launch_bounds__(256) tile_rows(const f4* __restrict__ x, long 
     }
 #pragma unroll
     for (int p = 0; p < 16; ++p) acc = fma((double)row[p].x, (double)row[p].y, acc);
+    if (MODE == 3 || MODE == 4 || MODE == 6) {
+      cur[t * 64 + lane] = cd < acc ? cd : acc;
+      if (MODE == 3 && lane == 0) tsum[t] = acc;
+    } else if (MODE == 7) {
+      __builtin_nontemporal_store(cd < acc ? cd : acc, cur + t * 64 + lane);
+    } else if (MODE == 5) {
+      acc += cd;
+    } else if (MODE == 8 || MODE == 9) {  // buffered: NB tiles' updates, then NB stores back to back
+      const int j = (int)(((t - t0) / tstep) % NB);
+      s_cur[wid][j][lane] = cd < acc ? cd : acc;
+      if (j == NB - 1 || t + tstep >= tend) {
+        __builtin_amdgcn_wave_barrier();
+        for (int q = 0; q <= j; ++q) cur[(t - (long)(j - q) * tstep) * 64 + lane] = s_cur[wid][q][lane];
+      }
+    }
     __builtin_amdgcn_wave_barrier();
   }
   if (acc == 1234.5) out[0] = 1.f;
@@ -208,6 +232,22 @@ int main(int argc, char** argv) {
     float t2 = timeit([&] { hipLaunchKernelGGL((tile_rows<2>), dim3(g4), dim3(256), 0, 0, x, ntiles, o); }, 10);
     printf("rows via LDS: %.0f GB/s (%.1f us)  rows direct: %.0f GB/s (%.1f us)\n", ntiles * 8192.0 / t1 / 1e6,
            t1 * 1e3, ntiles * 8192.0 / t2 / 1e6, t2 * 1e3);
+    double *cur, *tsum;
+    if (hipMalloc(&cur, ntiles * 64 * 8) || hipMalloc(&tsum, ntiles * 8)) return 1;
+    hipMemset(cur, 0, ntiles * 64 * 8);
+    float t3 = timeit([&] { hipLaunchKernelGGL((tile_rows<4>), dim3(g4), dim3(256), 0, 0, x, ntiles, o, cur, tsum); }, 10);
+    float t4 = timeit([&] { hipLaunchKernelGGL((tile_rows<3>), dim3(g4), dim3(256), 0, 0, x, ntiles, o, cur, tsum); }, 10);
+    const double b = ntiles * (8192.0 + 1024.0);  // rows + cur read + cur write
+    printf("rows via LDS + cur load/store: %.0f GB/s (%.1f us)  + tile-sum store: %.0f GB/s (%.1f us)\n",
+           b / t3 / 1e6, t3 * 1e3, b / t4 / 1e6, t4 * 1e3);
+    float t5 = timeit([&] { hipLaunchKernelGGL((tile_rows<5>), dim3(g4), dim3(256), 0, 0, x, ntiles, o, cur, tsum); }, 10);
+    float t6 = timeit([&] { hipLaunchKernelGGL((tile_rows<6>), dim3(g4), dim3(256), 0, 0, x, ntiles, o, cur, tsum); }, 10);
+    float t7 = timeit([&] { hipLaunchKernelGGL((tile_rows<7>), dim3(g4), dim3(256), 0, 0, x, ntiles, o, cur, tsum); }, 10);
+    printf("cur load only: %.1f us  cur store only: %.1f us  cur load + nt store: %.1f us\n", t5 * 1e3, t6 * 1e3,
+           t7 * 1e3);
+    float t8 = timeit([&] { hipLaunchKernelGGL((tile_rows<8>), dim3(g4), dim3(256), 0, 0, x, ntiles, o, cur, tsum); }, 10);
+    float t9 = timeit([&] { hipLaunchKernelGGL((tile_rows<9>), dim3(g4), dim3(256), 0, 0, x, ntiles, o, cur, tsum); }, 10);
+    printf("cur load + store buffered 4 tiles: %.1f us  8 tiles: %.1f us\n", t8 * 1e3, t9 * 1e3);
   }
   return 0;
 }
